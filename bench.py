@@ -1,0 +1,243 @@
+"""Benchmark: cell-updates/s of the graph-augmented NCA rollout on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json north_star): graph-augmented NCA, 16 channels, 72x72,
+torus offsets, r=4, K=8, update_hidden 128, fire_rate 0.5, pool batch B=1024 per GPU (the
+roofline headline configuration).  One benchmark "step" = one CA step over the whole batch.
+Per-step host work (the Python ``random.sample`` offset draw, same seed on every rank) is inside
+the timed region.  Weights: the reference's trained nca_latest.pt (carried by the committed golden
+fixture); state: synthetic (RGB, alpha ~ U(0,1), hidden ~ N(0,1)).  Fire masks come from the
+counter RNG keyed by global sample index, so the N-GPU run computes exactly the states the
+1-GPU run would for the same samples.
+
+Multi-GPU: one process per GPU (torchrun), B samples per rank (weak scaling), no collective on
+the data path; barrier + synchronize around the timed region, max time over ranks.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import platform
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+C, HD, D_MODEL, R, K = 16, 128, 16, 4, 8
+GAIN, THR, MSG_GAIN, FIRE = 0.05, 0.12, 0.25, 0.5
+FLOP_PER_CELL = 2 * (3 * C * HD + HD * C + C * C)      # 16,896 MFMA FLOP / cell-update
+BYTES_PER_CELL = 2 * C * 4                             # 128 B: read x, write x' (fp32)
+PEAK_F32_MFMA = 157.3e12                               # MI355X_MICROARCH.md, FP32 matrix
+PEAK_HBM = 8.0e12
+FIXTURE = os.path.join(ROOT, "tests", "golden", "graph_torus_latest_grown_b1_72.npz")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=96)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=1024, help="samples per GPU")
+    ap.add_argument("--size", type=int, default=72)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="wall budget of the CPU-baseline sample (rank 0, N=1 only)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def load_weights(dev):
+    z = np.load(FIXTURE, allow_pickle=False)
+    w = {k[2:]: torch.from_numpy(z[k]).to(dev) for k in z.files if k.startswith("w:")}
+    return w
+
+
+def weight_struct(w):
+    from graph_neural_cellular_automata_amd import step as S
+    t = dict(perception=w["perception.conv.weight"], w1=w["update_net.0.weight"],
+             b1=w["update_net.0.bias"], w2=w["update_net.2.weight"], gn_weight=w["norm.weight"],
+             gn_bias=w["norm.bias"], wq=w["graph.query_proj.weight"], bq=w["graph.query_proj.bias"],
+             wk=w["graph.key_proj.weight"], bk=w["graph.key_proj.bias"], wm=w["graph.msg_proj.weight"],
+             bm=w["graph.msg_proj.bias"], scaling=w["graph.scaling"])
+    return S.make_weights(t)
+
+
+def make_desc(B, H, W, offsets, rank, step0=0):
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    return S.make_desc(B=B, C=C, H=H, W=W, hidden=HD, d_model=D_MODEL, offsets=offsets,
+                       flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                       update_gain=GAIN, alpha_thr=THR, message_gain=MSG_GAIN, fire_rate=FIRE,
+                       fire_mode=L.FIRE_HASH, rng_seed=42, rng_step=step0, sample_base=rank * B)
+
+
+def cpu_baseline(budget_s: float):
+    """The numpy oracle (float32, the reference's arithmetic) on host cores: B=8 x 72^2 graph
+    steps until the wall budget is spent (>= 2 steps)."""
+    from oracle import nca_oracle as O
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(16, ncpu))
+    z = np.load(FIXTURE, allow_pickle=False)
+    p = {k[2:]: z[k].astype(np.float32) for k in z.files if k.startswith("w:")}
+    cfg = dict(update_gain=GAIN, alpha_thr=THR, use_groupnorm=True, graph=True,
+               message_gain=MSG_GAIN, hidden_only=True, zero_padded_shift=False, alive_to_alive=True)
+    rng = np.random.default_rng(0)
+    B, H = 8, 72
+    x = rng.random((B, C, H, H), dtype=np.float32)
+    x[:, 4:] = rng.standard_normal((B, C - 4, H, H), dtype=np.float32)
+    offs = O.build_offsets(R)
+    rr = random.Random(42)
+    ctx = threadpool_limits(limits=threads) if threadpool_limits else None
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        chosen = rr.sample(offs, K)
+        fm = O.hash_fire_mask(42, steps, 0, B, H, H, FIRE)
+        x = O.nca_step(x, p, cfg, chosen=chosen, fire_mask=fm)
+        steps += 1
+        el = time.perf_counter() - t0
+        if steps >= 2 and el >= budget_s:
+            break
+    if ctx is not None:
+        ctx.__exit__(None, None, None)
+    cpu = platform.processor() or platform.machine()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": B * H * H * steps / el, "unit": "cell-updates/s", "cores": threads,
+            "kind": "port",
+            "sample": f"numpy float32 oracle (oracle/nca_oracle.py), graph torus C16 72x72 K=8, "
+                      f"B={B}, {steps} steps in {el:.1f}s; BLAS threads={threads}, elementwise "
+                      f"single-threaded; host CPU: {cpu}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    lib = L.load()
+    from oracle.nca_oracle import build_offsets  # offset table only (row-major list)
+
+    B, H = args.batch, args.size
+    offsets_table = build_offsets(R)
+    w, keep = weight_struct(load_weights(dev))
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.rand(B, C, H, H, device=dev, generator=g)
+    x[:, 4:] = torch.randn(B, C - 4, H, H, device=dev, generator=g)
+    out = torch.empty_like(x)
+    scratch = torch.empty_like(x)
+    desc0 = make_desc(B, H, H, offsets_table[:K], rank)
+    ws = S.workspace(desc0, dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    rr = random.Random(42)  # same seed on every rank: identical offsets, no communication
+
+    def rollout(n, step0, src, dst):
+        flat = []
+        for _ in range(n):
+            for dy, dx in rr.sample(offsets_table, K):
+                flat += [dy, dx]
+        arr = (ctypes.c_int8 * len(flat))(*flat)
+        d = make_desc(B, H, H, offsets_table[:K], rank, step0)
+        rc = lib.gnca_rollout_f32(ctypes.byref(d), ctypes.byref(w), n, arr, src.data_ptr(),
+                                  dst.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(), sptr)
+        L.check(rc, "gnca_rollout_f32")
+
+    # warmup
+    if args.warmup > 0:
+        rollout(args.warmup, 0, x, out)
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rollout(args.steps, args.warmup, x, out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    cells = B * H * H
+    value = cells * args.steps * world / el
+
+    # --- K1 (dominant, MFMA-bound) average duration with HIP events on the launch stream ---
+    reps = 20
+    d = make_desc(B, H, H, rr.sample(offsets_table, K), rank, 0)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+    ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+    for r in range(reps):
+        ev[2 * r].record(stream)
+        L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), out.data_ptr(),
+                                         scratch.data_ptr(), None, None, ws.data_ptr(), ws.numel(),
+                                         sptr, L.PHASE_K1), "k1")
+        ev[2 * r + 1].record(stream)
+        ev2[2 * r].record(stream)
+        L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), out.data_ptr(),
+                                         scratch.data_ptr(), None, None, ws.data_ptr(), ws.numel(),
+                                         sptr, L.PHASE_K2), "k2")
+        ev2[2 * r + 1].record(stream)
+    torch.cuda.synchronize()
+    k1_ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(reps))[reps // 2]
+    k2_ms = sorted(ev2[2 * r].elapsed_time(ev2[2 * r + 1]) for r in range(reps))[reps // 2]
+    k1_flops = cells * FLOP_PER_CELL
+    k2_bytes = cells * C * 4 * 3                   # read x, dx; write x'
+    roof = {"bound": "mfma", "kernel": "gnca_k1_update<16,128>", "achieved": k1_flops / (k1_ms * 1e-3) / 1e12,
+            "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
+            "frac": k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA, "traffic": None,
+            "k1_ms": k1_ms, "flop_per_launch": k1_flops}
+    roof_k2 = {"bound": "hbm", "kernel": "gnca_k2_finalize", "achieved": k2_bytes / (k2_ms * 1e-3) / 1e9,
+               "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": k2_bytes / (k2_ms * 1e-3) / PEAK_HBM,
+               "k2_ms": k2_ms, "bytes_per_launch": k2_bytes}
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(args.cpu_seconds)
+        line = {
+            "metric": "cell-updates/sec (B·H·W·steps) for 16ch 72×72 rollout at 1/2/4/8 MI355X",
+            "value": value, "unit": "cell-updates/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic state (RGB,alpha~U(0,1), hidden~N(0,1)); trained nca_latest.pt "
+                    "weights from the committed golden fixture",
+            "config": {"workload": f"graph-augmented NCA rollout, torus, r={R}, K={K}, fire {FIRE}",
+                       "channels": C, "hidden": HD, "height": H, "width": H,
+                       "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}"},
+            "roofline": roof, "roofline_k2": roof_k2, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

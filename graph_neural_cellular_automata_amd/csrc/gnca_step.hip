@@ -1,0 +1,1134 @@
+// gnca_step.hip — MI355X (gfx950 / CDNA4) kernels for the NCA rollout step + the C ABI.
+//
+// One CA step (reference: src/modules/ncagraph.py:106-168, src/modules/nca.py:64-105,
+// src/modules/graph_augmentation.py:104-169, src/modules/perception.py:21-26) runs as:
+//
+//   K0  gnca_k0_offset_weights   zero-pad mode only: per-sample softmax weights over the
+//                                sampled offsets from per-row channel sums of x (the reference's
+//                                pooled Q.K logits, graph_augmentation.py:113-153, restated
+//                                exactly: Q and K enter only through their spatial means).
+//                                Torus mode needs no K0: mean(roll(K)) = mean(K), so every logit
+//                                is equal and the softmax weight is exactly 1/k.
+//   K1  gnca_k1_update<CP,HD>    persistent, one 256-thread workgroup per (sample, tile):
+//                                x tile + halo staged in LDS (torus-wrapped or zero-padded),
+//                                alive / sender planes, 3x3 depthwise perception, the offset
+//                                gather of ALIVE-MASKED x (the message projection is linear, so
+//                                W_M is applied once after the gather), the 1x1 MLP and the C x C
+//                                message projection on fp32 MFMA (v_mfma_f32_16x16x4_f32), message
+//                                policy, fire and pre-alive masks -> dx, plus per-tile fp64
+//                                GroupNorm partials (no atomics: deterministic).
+//   K2  gnca_k2_finalize         GroupNorm (per-sample stats combined in fixed order), tanh*gain,
+//                                residual, post-update alive gate on alpha (3x3 halo) -> x_out.
+//
+// MFMA fragment maps (v_mfma_f32_16x16x4_f32, lane l, g = l>>4, col = l&15):
+//   A[16x4]: lane supplies A[l&15][g];  B[4x16]: lane supplies B[g][l&15];
+//   D[16x16]: lane holds D[4g + r][l&15], r = 0..3.
+// A 16-cell group maps cell -> lane&15.  GEMM1 H[hid x cell] = W1[hid x 3C] Y[3C x cell]: lane
+// (cell, g) supplies feature slot 4s+g at k-step s, i.e. channels g, g+4, ... of its own cell,
+// so each lane computes its own perception features.  GEMM1's accumulator rows (hidden 4g+r of
+// tile m) are exactly the B operand of GEMM2 DL = W2 H at k-step (m, r) — no data movement.
+
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+#include <unordered_map>
+
+#include "gnca.h"
+
+namespace gnca {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr uint32_t kMsgOnly = 1u << 16;   // internal K1 flag: write agg message, skip MLP
+constexpr uint32_t kGraphOn = 1u << 17;   // internal K1 flag: gather + message projection needed
+
+__device__ __forceinline__ int wrapi(int v, int n) {
+  v %= n;
+  return v < 0 ? v + n : v;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Counter-based fire RNG (the build's definition; oracle/nca_oracle.py:hash_uniform).
+__device__ __forceinline__ float hash_uniform(uint64_t seed, int64_t step, uint64_t sample,
+                                              uint64_t cell) {
+  const uint64_t k = mix64(seed + 0x9E3779B97F4A7C15ull * (uint64_t)(uint32_t)(step + 1));
+  const uint64_t key = mix64(k ^ (sample << 32) ^ cell);
+  return (float)(key >> 40) * (1.0f / 16777216.0f);
+}
+
+// ------------------------------------------------------------------------------------------
+// LDS layout of K1 (floats; every region starts on a 16-byte boundary)
+// ------------------------------------------------------------------------------------------
+struct K1Layout {
+  int w1f, w2f, wmf, b1s, bms, percs, wts, red, xs, al, ap, sp, total;
+  int RH, RW, RWP, PSTR;
+};
+
+__host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
+__host__ __device__ inline int odd4(int v) {  // round up to 4*odd: conflict-free 16-lane b128
+  v = r4(v);
+  return ((v >> 2) & 1) ? v : v + 4;
+}
+
+__host__ __device__ inline K1Layout k1_layout(int CP, int HDP, int TH, int TW, int RY, int RX,
+                                              int kmax) {
+  K1Layout L;
+  const int CPQ = CP / 4, KS = 3 * CPQ, MT = HDP / 16, MO = (CP + 15) / 16;
+  const int KSP = odd4(KS), S2 = odd4(4 * MT), SWM = odd4(CPQ);
+  L.RH = TH + 2 * RY;
+  L.RW = TW + 2 * RX;
+  L.RWP = L.RW;
+  int pstr = L.RH * L.RWP;
+  pstr = (pstr + 31) & ~31;
+  pstr += 16;  // plane stride = 16 (mod 32): lanes 0-15 / 16-31 read different channels
+  L.PSTR = pstr;
+  int o = 0;
+  L.w1f = o; o += MT * 64 * KSP;
+  L.w2f = o; o += MO * 64 * S2;
+  L.wmf = o; o += MO * 64 * SWM;
+  L.b1s = o; o += r4(HDP);
+  L.bms = o; o += r4(CP);
+  L.percs = o; o += CP * 28;
+  L.wts = o; o += r4(kmax > 0 ? kmax : 1);
+  L.red = o; o += 4 * 8;  // 4 waves x (2 doubles + 2 floats + pad)
+  L.xs = o; o += CP * L.PSTR;
+  L.al = o; o += r4((L.RH + 2) * (L.RW + 2));
+  L.ap = o; o += r4(L.RH * L.RW);
+  L.sp = o; o += r4(L.RH * L.RW);
+  L.total = o;
+  return L;
+}
+
+struct K1Args {
+  const float* x;
+  float* out;          // dx (step) or agg message (message-only)
+  double* stats;       // [B * tps * 2]: per-tile (sum, sumsq) of dx
+  float* attn;         // [B,H,W] raw attention (or null)
+  float* attn_mm;      // [B * tps * 2]: per-tile (min, max) of raw attention
+  const float* perc;
+  const float* w1;
+  const float* b1;
+  const float* w2;
+  const float* wm;
+  const float* bm;
+  const float* offw;   // [B * k] per-sample offset weights, or null -> uniform_w
+  const void* fire;
+  uint64_t seed;
+  int64_t rng_step;
+  int64_t sample_base;
+  int B, C, H, W, hidden, k, RY, RX, TH, TW, tiles_x, tps, total_tiles, fire_mode;
+  float fire_rate, alpha_thr, graph_alpha_thr, message_gain, uniform_w;
+  uint32_t flags;
+  int8_t offs[2 * GNCA_MAX_OFFSETS];
+};
+
+template <int CP, int HDP>
+__global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int CPQ = CP / 4, KS = 3 * CPQ, MT = HDP / 16, MO = (CP + 15) / 16;
+  constexpr int KSP = ((((KS + 3) & ~3) >> 2) & 1) ? ((KS + 3) & ~3) : ((KS + 3) & ~3) + 4;
+  constexpr int S2r = 4 * MT;
+  constexpr int S2 = ((S2r >> 2) & 1) ? S2r : S2r + 4;
+  constexpr int SWMr = (CPQ + 3) & ~3;
+  constexpr int SWM = ((SWMr >> 2) & 1) ? SWMr : SWMr + 4;
+
+  const K1Layout L = k1_layout(CP, HDP, a.TH, a.TW, a.RY, a.RX, a.k);
+  float* w1f = smem + L.w1f;
+  float* w2f = smem + L.w2f;
+  float* wmf = smem + L.wmf;
+  float* b1s = smem + L.b1s;
+  float* bms = smem + L.bms;
+  float* percs = smem + L.percs;
+  float* wts = smem + L.wts;
+  float* red = smem + L.red;
+  float* xs = smem + L.xs;
+  float* al = smem + L.al;
+  float* ap = smem + L.ap;
+  float* sp = smem + L.sp;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int C = a.C, H = a.H, W = a.W, Hd = a.hidden;
+  const bool msg_only = (a.flags & kMsgOnly) != 0;
+  const bool graph_on = (a.flags & kGraphOn) != 0;
+  const bool zp = (a.flags & GNCA_ZERO_PAD_SHIFT) != 0;
+  const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
+  const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
+  const bool want_attn = (a.flags & GNCA_ATTENTION) != 0;
+  const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
+
+  // ---- weights -> LDS in MFMA fragment order (once per persistent workgroup) ----
+  if (!msg_only) {
+    for (int idx = tid; idx < MT * 64 * KSP; idx += kThreads) {
+      const int s = idx % KSP, ml = idx / KSP, l = ml & 63, m = ml >> 6;
+      const int hid = 16 * m + (l & 15), slot = 4 * s + (l >> 4);
+      const int f = slot / CP, c = slot - f * CP;
+      float v = 0.f;
+      if (s < KS && hid < Hd && c < C) v = a.w1[(size_t)hid * 3 * C + f * C + c];
+      w1f[idx] = v;
+    }
+    for (int idx = tid; idx < MO * 64 * S2; idx += kThreads) {
+      const int e = idx % S2, ml = idx / S2, l = ml & 63, mo = ml >> 6;
+      const int m = e >> 2, r = e & 3;
+      const int co = 16 * mo + (l & 15), hid = 16 * m + 4 * (l >> 4) + r;
+      float v = 0.f;
+      if (e < S2r && co < C && hid < Hd) v = a.w2[(size_t)co * Hd + hid];
+      w2f[idx] = v;
+    }
+    for (int idx = tid; idx < HDP; idx += kThreads) b1s[idx] = idx < Hd ? a.b1[idx] : 0.f;
+    for (int idx = tid; idx < CP * 28; idx += kThreads) {
+      const int c = idx / 28, e = idx % 28;
+      percs[idx] = (c < C && e < 27) ? a.perc[(3 * c + e / 9) * 9 + e % 9] : 0.f;
+    }
+  }
+  if (graph_on) {
+    for (int idx = tid; idx < MO * 64 * SWM; idx += kThreads) {
+      const int s = idx % SWM, ml = idx / SWM, l = ml & 63, mo = ml >> 6;
+      const int co = 16 * mo + (l & 15), c = 4 * s + (l >> 4);
+      wmf[idx] = (s < CPQ && co < C && c < C) ? a.wm[co * C + c] : 0.f;
+    }
+    for (int idx = tid; idx < CP; idx += kThreads) bms[idx] = idx < C ? a.bm[idx] : 0.f;
+  }
+
+  const int RH = L.RH, RW = L.RW, RWP = L.RWP, PSTR = L.PSTR;
+  const int RY = a.RY, RX = a.RX, TH = a.TH, TW = a.TW;
+  const int ncell = TH * TW, ngroups = (ncell + 15) >> 4;
+  const size_t HW = (size_t)H * W;
+
+  for (int tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+    const int b = tile / a.tps, tin = tile - b * a.tps;
+    const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+    const int i0 = ty * TH, j0 = tx * TW;
+    const float* xb = a.x + (size_t)b * C * HW;
+    __syncthreads();  // previous tile's LDS readers are done
+
+    // ---- stage x region (halo RY x RX), torus-wrapped or zero outside the image ----
+    const int need_x = graph_on ? CP : (msg_only ? 0 : CP);
+    for (int idx = tid; idx < need_x * RH * RW; idx += kThreads) {
+      const int c = idx / (RH * RW), rem = idx - c * RH * RW;
+      const int vr = rem / RW, vc = rem - vr * RW;
+      int ii = i0 - RY + vr, jj = j0 - RX + vc;
+      float v = 0.f;
+      if (c < C) {
+        if (zp) {
+          if (ii >= 0 && ii < H && jj >= 0 && jj < W) v = xb[c * HW + (size_t)ii * W + jj];
+        } else {
+          ii = wrapi(ii, H);
+          jj = wrapi(jj, W);
+          v = xb[c * HW + (size_t)ii * W + jj];
+        }
+      }
+      xs[c * PSTR + vr * RWP + vc] = v;
+    }
+    // ---- alpha region (one more ring) ----
+    for (int idx = tid; idx < (RH + 2) * (RW + 2); idx += kThreads) {
+      const int vr = idx / (RW + 2), vc = idx - vr * (RW + 2);
+      int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
+      float v = 0.f;
+      if (zp) {
+        if (ii >= 0 && ii < H && jj >= 0 && jj < W) v = xb[3 * HW + (size_t)ii * W + jj];
+      } else {
+        v = xb[3 * HW + (size_t)wrapi(ii, H) * W + wrapi(jj, W)];
+      }
+      al[idx] = v;
+    }
+    if (graph_on)
+      for (int o = tid; o < a.k; o += kThreads) wts[o] = a.offw ? a.offw[(size_t)b * a.k + o] : a.uniform_w;
+    __syncthreads();
+
+    // ---- alive plane A (max_pool 3x3 > thr, image-bounded, ncagraph.py:85-92) and the
+    //      sender plane (alive_to_alive ? A : 1), zero where the source is off-image (pad) ----
+    for (int idx = tid; idx < RH * RW; idx += kThreads) {
+      const int vr = idx / RW, vc = idx - vr * RW;
+      int iq = i0 - RY + vr, jq = j0 - RX + vc;
+      bool in_img = true;
+      if (zp) in_img = iq >= 0 && iq < H && jq >= 0 && jq < W;
+      else { iq = wrapi(iq, H); jq = wrapi(jq, W); }
+      float A = 0.f, As = 0.f;
+      if (in_img) {
+        float mx = -INFINITY;
+        for (int dv = -1; dv <= 1; ++dv) {
+          if (iq + dv < 0 || iq + dv >= H) continue;
+          for (int du = -1; du <= 1; ++du) {
+            if (jq + du < 0 || jq + du >= W) continue;
+            mx = fmaxf(mx, al[(vr + 1 + dv) * (RW + 2) + (vc + 1 + du)]);
+          }
+        }
+        A = mx > thr ? 1.f : 0.f;
+        As = mx > gthr ? 1.f : 0.f;
+      }
+      ap[idx] = A;
+      sp[idx] = a2a ? As : (in_img ? 1.f : 0.f);
+    }
+    __syncthreads();
+
+    double s1 = 0.0, s2 = 0.0;
+    float amin = INFINITY, amax = -INFINITY;
+
+    for (int q = wave; q < ngroups; q += kThreads / 64) {
+      const int n = 16 * q + c16;
+      int ti = n / TW, tj = n - (n / TW) * TW;
+      const int i = i0 + ti, j = j0 + tj;
+      const bool valid = n < ncell && i < H && j < W;
+      if (!valid) { ti = 0; tj = 0; }
+      const int vr = RY + ti, vc = RX + tj;
+      const int ic = valid ? i : i0, jc = valid ? j : j0;
+
+      // -- graph gather of alive-masked x (linear message: W_M applied after the sum) --
+      float gv[CPQ];
+#pragma unroll
+      for (int t = 0; t < CPQ; ++t) gv[t] = 0.f;
+      float S = 0.f;
+      if (graph_on) {
+        for (int o = 0; o < a.k; ++o) {
+          const int dy = a.offs[2 * o], dxo = a.offs[2 * o + 1];
+          const int qr = vr - dy, qc = zp ? vc : vc - dxo;
+          const float wsp = wts[o] * sp[qr * RW + qc];
+          S += wsp;
+          const float* xq = xs + g * PSTR + qr * RWP + qc;
+#pragma unroll
+          for (int t = 0; t < CPQ; ++t) gv[t] += wsp * xq[4 * t * PSTR];
+        }
+      }
+      f4 accm[MO];
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo) accm[mo] = f4{0.f, 0.f, 0.f, 0.f};
+      if (graph_on) {
+#pragma unroll
+        for (int s = 0; s < CPQ; ++s)
+#pragma unroll
+          for (int mo = 0; mo < MO; ++mo)
+            accm[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wmf[(mo * 64 + lane) * SWM + s], gv[s],
+                                                            accm[mo], 0, 0, 0);
+      }
+
+      // -- attention map: sum_o w_o/C * sum_c |A(q) (W_M x(q) + b_M)_c|  (graph_aug.py:160-162) --
+      if (want_attn && graph_on) {
+        float att = 0.f;
+        for (int o = 0; o < a.k; ++o) {
+          const int dy = a.offs[2 * o], dxo = a.offs[2 * o + 1];
+          const int qr = vr - dy, qc = zp ? vc : vc - dxo;
+          const float* xq = xs + g * PSTR + qr * RWP + qc;
+          f4 tmp[MO];
+#pragma unroll
+          for (int mo = 0; mo < MO; ++mo) tmp[mo] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < CPQ; ++s)
+#pragma unroll
+            for (int mo = 0; mo < MO; ++mo)
+              tmp[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wmf[(mo * 64 + lane) * SWM + s],
+                                                             xq[4 * s * PSTR], tmp[mo], 0, 0, 0);
+          float part = 0.f;
+#pragma unroll
+          for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int c = 16 * mo + 4 * g + r;
+              if (c < C) part += fabsf(tmp[mo][r] + bms[c]);
+            }
+          part += __shfl_xor(part, 16);
+          part += __shfl_xor(part, 32);
+          att += wts[o] * sp[qr * RW + qc] / (float)C * part;
+        }
+        if (valid) {
+          if (g == 0) a.attn[(size_t)b * HW + (size_t)i * W + j] = att;
+          amin = fminf(amin, att);
+          amax = fmaxf(amax, att);
+        }
+      }
+
+      if (msg_only) {
+        // agg_message = W_M gather + b_M * sum_o w_o A(q_o)  (no policy, no masks)
+#pragma unroll
+        for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = 16 * mo + 4 * g + r;
+            if (valid && c < C)
+              a.out[((size_t)b * C + c) * HW + (size_t)i * W + j] = accm[mo][r] + bms[c] * S;
+          }
+        continue;
+      }
+
+      // -- perception: 3x3 depthwise cross-correlation, zero padding (perception.py:16-25) --
+      float y[KS];
+      {
+        const bool up = ic > 0, dn = ic < H - 1, lf = jc > 0, rt = jc < W - 1;
+#pragma unroll
+        for (int t = 0; t < CPQ; ++t) {
+          const int c = 4 * t + g;
+          const float* xc = xs + c * PSTR + vr * RWP + vc;
+          float nb[9];
+          nb[0] = (up && lf) ? xc[-RWP - 1] : 0.f;
+          nb[1] = up ? xc[-RWP] : 0.f;
+          nb[2] = (up && rt) ? xc[-RWP + 1] : 0.f;
+          nb[3] = lf ? xc[-1] : 0.f;
+          nb[4] = xc[0];
+          nb[5] = rt ? xc[1] : 0.f;
+          nb[6] = (dn && lf) ? xc[RWP - 1] : 0.f;
+          nb[7] = dn ? xc[RWP] : 0.f;
+          nb[8] = (dn && rt) ? xc[RWP + 1] : 0.f;
+          const f4* pw = reinterpret_cast<const f4*>(percs + c * 28);
+          float wv[28];
+#pragma unroll
+          for (int e = 0; e < 7; ++e) {
+            const f4 q4 = pw[e];
+            wv[4 * e] = q4[0]; wv[4 * e + 1] = q4[1]; wv[4 * e + 2] = q4[2]; wv[4 * e + 3] = q4[3];
+          }
+#pragma unroll
+          for (int f = 0; f < 3; ++f) {
+            float acc = 0.f;
+#pragma unroll
+            for (int e = 0; e < 9; ++e) acc = fmaf(wv[9 * f + e], nb[e], acc);
+            y[f * CPQ + t] = acc;
+          }
+        }
+      }
+
+      // -- GEMM1: H = W1 . Y  (fp32 MFMA, 16 hidden x 16 cells per tile) --
+      f4 acc[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s0 = 0; s0 < KS; s0 += 4) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const f4 w4 = *reinterpret_cast<const f4*>(w1f + (m * 64 + lane) * KSP + s0);
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (s0 + u < KS)
+              acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[u], y[s0 + u], acc[m], 0, 0, 0);
+        }
+      }
+      // -- bias + ReLU, GEMM2: DL = W2 . H  (accumulator rows are GEMM2's B operand) --
+      f4 acc2[MO];
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo) acc2[mo] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const f4 bb = *reinterpret_cast<const f4*>(b1s + 16 * m + 4 * g);
+        f4 w2v[MO];
+#pragma unroll
+        for (int mo = 0; mo < MO; ++mo)
+          w2v[mo] = *reinterpret_cast<const f4*>(w2f + (mo * 64 + lane) * S2 + 4 * m);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float h = fmaxf(acc[m][r] + bb[r], 0.f);
+#pragma unroll
+          for (int mo = 0; mo < MO; ++mo)
+            acc2[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2v[mo][r], h, acc2[mo], 0, 0, 0);
+        }
+      }
+
+      // -- masks: stochastic fire (ncagraph.py:144-146), pre-update alive (:149-150) --
+      float keep = ap[vr * RW + vc];
+      if (a.fire_mode != GNCA_FIRE_NONE) {
+        const size_t cell = (size_t)ic * W + jc;
+        bool fire;
+        if (a.fire_mode == GNCA_FIRE_RAND_F32)
+          fire = reinterpret_cast<const float*>(a.fire)[(size_t)b * HW + cell] <= a.fire_rate;
+        else if (a.fire_mode == GNCA_FIRE_MASK_U8)
+          fire = reinterpret_cast<const uint8_t*>(a.fire)[(size_t)b * HW + cell] != 0;
+        else
+          fire = hash_uniform(a.seed, a.rng_step, (uint64_t)(a.sample_base + b), cell) <= a.fire_rate;
+        if (!fire) keep = 0.f;
+      }
+      // -- epilogue: dx = dl + tanh(m)*message_gain (hidden_only), masked --
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 16 * mo + 4 * g + r;
+          if (!valid || c >= C) continue;
+          float v = acc2[mo][r];
+          if (graph_on && !(hidden_only && c < 4))
+            v += tanhf(accm[mo][r] + bms[c] * S) * a.message_gain;
+          v = keep != 0.f ? v : 0.f;
+          a.out[((size_t)b * C + c) * HW + (size_t)i * W + j] = v;
+          s1 += (double)v;
+          s2 += (double)v * (double)v;
+        }
+    }
+
+    // ---- per-tile partials: wave shuffle, then across the 4 waves in LDS ----
+    if (!msg_only) {
+      for (int off = 32; off > 0; off >>= 1) {
+        s1 += __shfl_xor(s1, off);
+        s2 += __shfl_xor(s2, off);
+      }
+    }
+    if (want_attn) {
+      for (int off = 32; off > 0; off >>= 1) {
+        amin = fminf(amin, __shfl_xor(amin, off));
+        amax = fmaxf(amax, __shfl_xor(amax, off));
+      }
+    }
+    double* redd = reinterpret_cast<double*>(red);
+    if (lane == 0) {
+      redd[wave * 2 + 0] = s1;
+      redd[wave * 2 + 1] = s2;
+      red[16 + wave * 2 + 0] = amin;
+      red[16 + wave * 2 + 1] = amax;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      if (!msg_only) {
+        double t1 = 0.0, t2 = 0.0;
+        for (int w = 0; w < kThreads / 64; ++w) { t1 += redd[w * 2]; t2 += redd[w * 2 + 1]; }
+        a.stats[(size_t)tile * 2 + 0] = t1;
+        a.stats[(size_t)tile * 2 + 1] = t2;
+      }
+      if (want_attn) {
+        float mn = INFINITY, mx = -INFINITY;
+        for (int w = 0; w < kThreads / 64; ++w) {
+          mn = fminf(mn, red[16 + w * 2]);
+          mx = fmaxf(mx, red[16 + w * 2 + 1]);
+        }
+        a.attn_mm[(size_t)tile * 2 + 0] = mn;
+        a.attn_mm[(size_t)tile * 2 + 1] = mx;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K2: GroupNorm + tanh*gain + residual + post-update alpha gate
+// ------------------------------------------------------------------------------------------
+struct K2Args {
+  const float* x;
+  const float* dx;
+  float* out;
+  const double* stats;   // [B * tps * 2]
+  const float* gamma;
+  const float* beta;
+  float* attn;           // normalise in place if non-null
+  const float* attn_mm;  // [B * tps * 2]
+  int B, C, H, W, tps, TH2, TW2, tiles2_x, tps2, total2;
+  float gain, thr, eps;
+  int use_gn;
+};
+
+__global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float sh_norm[4];
+  const int tid = threadIdx.x;
+  const int tile = blockIdx.x;
+  const int b = tile / a.tps2, tin = tile - b * a.tps2;
+  const int ty = tin / a.tiles2_x, tx = tin - ty * a.tiles2_x;
+  const int i0 = ty * a.TH2, j0 = tx * a.TW2;
+  const int C = a.C, H = a.H, W = a.W;
+  const size_t HW = (size_t)H * W;
+
+  if (tid == 0) {
+    float mu = 0.f, rs = 1.f;
+    if (a.use_gn) {
+      double t1 = 0.0, t2 = 0.0;  // fixed order: deterministic
+      for (int t = 0; t < a.tps; ++t) {
+        t1 += a.stats[((size_t)b * a.tps + t) * 2];
+        t2 += a.stats[((size_t)b * a.tps + t) * 2 + 1];
+      }
+      const double n = (double)C * (double)HW;
+      const double m = t1 / n;
+      double var = t2 / n - m * m;
+      if (var < 0.0) var = 0.0;
+      mu = (float)m;
+      rs = (float)(1.0 / sqrt(var + (double)a.eps));
+    }
+    float amn = 0.f, amx = 0.f;
+    if (a.attn) {
+      amn = INFINITY; amx = -INFINITY;
+      for (int t = 0; t < a.tps; ++t) {
+        amn = fminf(amn, a.attn_mm[((size_t)b * a.tps + t) * 2]);
+        amx = fmaxf(amx, a.attn_mm[((size_t)b * a.tps + t) * 2 + 1]);
+      }
+    }
+    sh_norm[0] = mu; sh_norm[1] = rs; sh_norm[2] = amn; sh_norm[3] = amx;
+  }
+  __syncthreads();
+  const float mu = sh_norm[0], rs = sh_norm[1];
+  const float* xb = a.x + (size_t)b * C * HW;
+  const float* db = a.dx + (size_t)b * C * HW;
+  float* ob = a.out + (size_t)b * C * HW;
+  const float g3 = a.use_gn ? a.gamma[3] : 1.f, b3 = a.use_gn ? a.beta[3] : 0.f;
+
+  // updated alpha over the tile + 1-cell ring (-inf off-image: max_pool padding)
+  const int AW = a.TW2 + 2, AH = a.TH2 + 2;
+  float* at = smem;
+  for (int idx = tid; idx < AW * AH; idx += kThreads) {
+    const int r = idx / AW, c = idx - r * AW;
+    const int ii = i0 - 1 + r, jj = j0 - 1 + c;
+    float v = -INFINITY;
+    if (ii >= 0 && ii < H && jj >= 0 && jj < W) {
+      const size_t p = 3 * HW + (size_t)ii * W + jj;
+      float d = db[p];
+      if (a.use_gn) d = (d - mu) * rs * g3 + b3;
+      v = xb[p] + tanhf(d) * a.gain;
+    }
+    at[idx] = v;
+  }
+  __syncthreads();
+
+  const int ncell = a.TH2 * a.TW2;
+  for (int n = tid; n < ncell; n += kThreads) {
+    const int ti = n / a.TW2, tj = n - ti * a.TW2;
+    const int i = i0 + ti, j = j0 + tj;
+    if (i >= H || j >= W) continue;
+    const size_t cell = (size_t)i * W + j;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int dv = 0; dv < 3; ++dv)
+#pragma unroll
+      for (int du = 0; du < 3; ++du) mx = fmaxf(mx, at[(ti + dv) * AW + tj + du]);
+    const float post = mx > a.thr ? 1.f : 0.f;
+    for (int c = 0; c < C; ++c) {
+      const size_t p = c * HW + cell;
+      float v;
+      if (c == 3) {
+        v = at[(ti + 1) * AW + tj + 1] * post;
+      } else {
+        float d = db[p];
+        if (a.use_gn) d = (d - mu) * rs * a.gamma[c] + a.beta[c];
+        v = xb[p] + tanhf(d) * a.gain;
+      }
+      ob[p] = v;
+    }
+    if (a.attn) {
+      const float amn = sh_norm[2], amx = sh_norm[3];
+      float* ap = a.attn + (size_t)b * HW + cell;
+      *ap = (*ap - amn) / (amx - amn + 1e-8f);
+    }
+  }
+}
+
+// normalise a message-only attention map (no K2 in message mode)
+__global__ __launch_bounds__(kThreads) void gnca_attn_normalize(float* attn, const float* attn_mm,
+                                                                int tps, int HW) {
+  const int b = blockIdx.y;
+  __shared__ float mm[2];
+  if (threadIdx.x == 0) {
+    float mn = INFINITY, mx = -INFINITY;
+    for (int t = 0; t < tps; ++t) {
+      mn = fminf(mn, attn_mm[((size_t)b * tps + t) * 2]);
+      mx = fmaxf(mx, attn_mm[((size_t)b * tps + t) * 2 + 1]);
+    }
+    mm[0] = mn; mm[1] = mx;
+  }
+  __syncthreads();
+  for (int p = blockIdx.x * kThreads + threadIdx.x; p < HW; p += gridDim.x * kThreads) {
+    float* q = attn + (size_t)b * HW + p;
+    *q = (*q - mm[0]) / (mm[1] - mm[0] + 1e-8f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K0: zero-pad offset weights.  logit_o = qbar . kbar_o with
+//   qbar   = W_Q xbar + b_Q                              (mean of Q over the image)
+//   kbar_o = (W_K S_o + b_K * n_o W) / (H W)             (mean of the row-shifted, zero-padded K)
+// where S_o sums the per-row channel sums of x over the rows that stay inside the image and n_o
+// counts them; softmax over offsets with temperature |scaling| + 1e-6.  fp64 throughout.
+// ------------------------------------------------------------------------------------------
+struct K0Args {
+  const float* x;
+  const float* wq;
+  const float* bq;
+  const float* wk;
+  const float* bk;
+  const float* scaling;
+  float* offw;  // [B * k]
+  int B, C, H, W, d, k;
+  int8_t offs[2 * GNCA_MAX_OFFSETS];
+};
+
+__global__ __launch_bounds__(kThreads) void gnca_k0_offset_weights(const K0Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  double* rs = reinterpret_cast<double*>(smem);         // [C][H] row sums
+  double* xbar = rs + (size_t)a.C * a.H;                 // [C]
+  double* qbar = xbar + a.C;                             // [d]
+  double* logit = qbar + a.d;                            // [k]
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int C = a.C, H = a.H, W = a.W;
+  const size_t HW = (size_t)H * W;
+  const float* xb = a.x + (size_t)b * C * HW;
+  const int lane = tid & 63, wave = tid >> 6;
+  // one wave per (c, row): lanes stride the row, fixed-order shuffle tree
+  for (int cr = wave; cr < C * H; cr += kThreads / 64) {
+    const int c = cr / H, r = cr - c * H;
+    double s = 0.0;
+    for (int j = lane; j < W; j += 64) s += (double)xb[c * HW + (size_t)r * W + j];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) rs[cr] = s;
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kThreads) {
+    double s = 0.0;
+    for (int r = 0; r < H; ++r) s += rs[c * H + r];
+    xbar[c] = s / (double)HW;
+  }
+  __syncthreads();
+  for (int e = tid; e < a.d; e += kThreads) {
+    double s = (double)a.bq[e];
+    for (int c = 0; c < C; ++c) s += (double)a.wq[e * C + c] * xbar[c];
+    qbar[e] = s;
+  }
+  __syncthreads();
+  for (int o = tid; o < a.k; o += kThreads) {
+    const int dy = a.offs[2 * o];
+    const int lo = dy > 0 ? 0 : -dy, hi = dy > 0 ? H - dy : H;  // valid source rows [lo,hi)
+    const int nrows = hi > lo ? hi - lo : 0;
+    double L = 0.0;
+    for (int e = 0; e < a.d; ++e) {
+      double kk = (double)a.bk[e] * (double)nrows * (double)W;
+      for (int c = 0; c < C; ++c) {
+        double S = 0.0;
+        for (int r = lo; r < hi; ++r) S += rs[c * H + r];
+        kk += (double)a.wk[e * C + c] * S;
+      }
+      L += qbar[e] * (kk / (double)HW);
+    }
+    logit[o] = L;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double mx = -INFINITY;
+    for (int o = 0; o < a.k; ++o) mx = fmax(mx, logit[o]);
+    const double T = fabs((double)a.scaling[0]) + 1e-6;
+    double sum = 0.0;
+    for (int o = 0; o < a.k; ++o) {
+      logit[o] = exp((logit[o] - mx) / T);
+      sum += logit[o];
+    }
+    for (int o = 0; o < a.k; ++o) a.offw[(size_t)b * a.k + o] = (float)(logit[o] / sum);
+  }
+}
+
+// FixedSobelPerception.forward alone: y[:, f*C + c] = sum_ab w[3c+f][a][b] x(i+a-1, j+b-1).
+__global__ __launch_bounds__(kThreads) void gnca_perceive(int B, int C, int H, int W,
+                                                          const float* w, const float* x, float* y) {
+  const size_t HW = (size_t)H * W;
+  const size_t total = (size_t)B * C * HW;
+  for (size_t idx = (size_t)blockIdx.x * kThreads + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * kThreads) {
+    const size_t b = idx / (C * HW), rem = idx - b * C * HW;
+    const int c = (int)(rem / HW);
+    const size_t cell = rem - (size_t)c * HW;
+    const int i = (int)(cell / W), j = (int)(cell - (size_t)i * W);
+    const float* xc = x + (b * C + c) * HW;
+    float nb[9];
+    for (int dv = 0; dv < 3; ++dv)
+      for (int du = 0; du < 3; ++du) {
+        const int ii = i + dv - 1, jj = j + du - 1;
+        nb[dv * 3 + du] = (ii >= 0 && ii < H && jj >= 0 && jj < W) ? xc[(size_t)ii * W + jj] : 0.f;
+      }
+    for (int f = 0; f < 3; ++f) {
+      float acc = 0.f;
+      for (int e = 0; e < 9; ++e) acc = fmaf(w[(3 * c + f) * 9 + e], nb[e], acc);
+      y[(b * 3 * C + (size_t)f * C + c) * HW + cell] = acc;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------
+thread_local int g_last_hip = 0;
+
+typedef void (*k1_fn)(K1Args);
+
+struct Variant {
+  int CP, HDP;
+  const void* fn;
+};
+
+#define GNCA_VARIANT(cp, hd) {cp, hd, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd>)}
+static const Variant kVariants[] = {
+    GNCA_VARIANT(4, 32),   GNCA_VARIANT(4, 64),   GNCA_VARIANT(4, 128),
+    GNCA_VARIANT(8, 32),   GNCA_VARIANT(8, 64),   GNCA_VARIANT(8, 128),
+    GNCA_VARIANT(12, 64),  GNCA_VARIANT(12, 128), GNCA_VARIANT(16, 32),
+    GNCA_VARIANT(16, 64),  GNCA_VARIANT(16, 128), GNCA_VARIANT(16, 256),
+    GNCA_VARIANT(20, 128), GNCA_VARIANT(24, 128), GNCA_VARIANT(28, 128),
+    GNCA_VARIANT(32, 64),  GNCA_VARIANT(32, 128),
+};
+#undef GNCA_VARIANT
+
+static const Variant* find_variant(int C, int Hd) {
+  const int CP = (C + 3) & ~3;
+  const Variant* best = nullptr;
+  for (const Variant& v : kVariants)
+    if (v.CP == CP && v.HDP >= Hd && (!best || v.HDP < best->HDP)) best = &v;
+  return best;
+}
+
+struct Plan {
+  const Variant* var;
+  int k, RY, RX, TH, TW, tiles_x, tiles_y, tps, total_tiles;
+  size_t lds1;
+  bool graph_on, need_k0;
+  // K2
+  int TH2, TW2, tiles2_x, tps2, total2;
+  size_t lds2;
+  // workspace carve (bytes)
+  size_t off_dx, off_stats, off_mm, off_offw, ws_bytes;
+};
+
+static int max_lds_bytes() { return 160 * 1024; }
+
+static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
+  if (!d || d->B <= 0 || d->C < 4 || d->H <= 0 || d->W <= 0 || d->hidden <= 0) return false;
+  if (d->num_offsets < 0 || d->num_offsets > GNCA_MAX_OFFSETS) return false;
+  const bool graph = (d->flags & GNCA_GRAPH) != 0;
+  if (graph && d->d_model <= 0) return false;
+  P->var = find_variant(d->C, d->hidden);
+  if (!P->var) return false;
+  P->k = graph ? d->num_offsets : 0;
+  const bool attn = graph && (d->flags & GNCA_ATTENTION);
+  P->graph_on = graph && P->k > 0 && (msg_only || attn || d->message_gain != 0.f);
+  const bool zp = (d->flags & GNCA_ZERO_PAD_SHIFT) != 0;
+  P->need_k0 = P->graph_on && zp;
+  int ry = 1, rx = 1;
+  if (P->graph_on)
+    for (int o = 0; o < P->k; ++o) {
+      const int dy = d->offsets[2 * o], dx = d->offsets[2 * o + 1];
+      ry = ry > abs(dy) ? ry : abs(dy);
+      if (!zp) rx = rx > abs(dx) ? rx : abs(dx);
+    }
+  P->RY = ry;
+  P->RX = rx;
+  const int CP = P->var->CP, HDP = P->var->HDP;
+  // tile choice: fewest padded cells + staged halo, LDS <= 80 KB (2 workgroups / CU) if possible
+  static const int ths[] = {4, 8, 12, 16, 24};
+  static const int tws[] = {8, 12, 16, 24, 32, 48, 64};
+  double best = 1e300;
+  int bth = 0, btw = 0;
+  size_t blds = 0;
+  for (int pass = 0; pass < 2 && !bth; ++pass) {
+    const size_t cap = pass == 0 ? 80 * 1024 : (size_t)max_lds_bytes();
+    for (int th : ths)
+      for (int tw : tws) {
+        if ((th * tw) % 16) continue;
+        const K1Layout L = k1_layout(CP, HDP, th, tw, ry, rx, P->k);
+        const size_t bytes = (size_t)L.total * 4;
+        if (bytes > cap) continue;
+        const long tx = (d->W + tw - 1) / tw, ty = (d->H + th - 1) / th;
+        const double cells = (double)tx * ty * th * tw;
+        const double stage = (double)tx * ty * (th + 2 * ry) * (tw + 2 * rx) * CP;
+        const double cost = cells * (msg_only ? 0.1 : 1.0) + 0.004 * stage + 30.0 * tx * ty;
+        if (cost < best) { best = cost; bth = th; btw = tw; blds = bytes; }
+      }
+  }
+  if (!bth) return false;
+  P->TH = bth;
+  P->TW = btw;
+  P->lds1 = blds;
+  P->tiles_x = (d->W + btw - 1) / btw;
+  P->tiles_y = (d->H + bth - 1) / bth;
+  P->tps = P->tiles_x * P->tiles_y;
+  P->total_tiles = P->tps * d->B;
+  // K2 tiles: full rows up to 128 wide
+  P->TW2 = d->W <= 128 ? d->W : 128;
+  P->TH2 = 8;
+  P->tiles2_x = (d->W + P->TW2 - 1) / P->TW2;
+  P->tps2 = P->tiles2_x * ((d->H + P->TH2 - 1) / P->TH2);
+  P->total2 = P->tps2 * d->B;
+  P->lds2 = (size_t)(P->TH2 + 2) * (P->TW2 + 2) * 4;
+  // workspace
+  size_t o = 0;
+  auto carve = [&o](size_t bytes) { size_t at = o; o += (bytes + 255) & ~(size_t)255; return at; };
+  const size_t n = (size_t)d->B * d->C * d->H * d->W;
+  P->off_dx = carve(msg_only ? 0 : n * 4);
+  P->off_stats = carve((size_t)P->total_tiles * 2 * sizeof(double));
+  P->off_mm = carve((size_t)P->total_tiles * 2 * sizeof(float));
+  P->off_offw = carve((size_t)d->B * (P->k > 0 ? P->k : 1) * sizeof(float));
+  P->ws_bytes = o;
+  if (P->need_k0) {
+    const size_t k0 = ((size_t)d->C * d->H + d->C + d->d_model + P->k) * sizeof(double);
+    if (k0 > 64 * 1024) return false;
+  }
+  return true;
+}
+
+struct DevInfo {
+  int cus = 256;
+};
+
+static int device_cus() {
+  static std::mutex mu;
+  static std::unordered_map<int, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int cus = 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  cache[dev] = cus;
+  return cus;
+}
+
+static int occupancy(const void* fn, size_t lds) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, std::unordered_map<size_t, int>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& m = cache[fn];
+  auto it = m.find(lds);
+  if (it != m.end()) return it->second;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, lds) != hipSuccess || n <= 0) n = 1;
+  if (n > 8) n = 8;
+  m[lds] = n;
+  return n;
+}
+
+static int check_launch() {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_last_hip = (int)e;
+    return GNCA_ERR_HIP;
+  }
+  return GNCA_OK;
+}
+
+static void fill_k1(K1Args& k1, const gnca_step_desc* d, const gnca_weights* w, const Plan& P,
+                    const float* x, float* out, const void* fire, float* attn, char* ws) {
+  memset(&k1, 0, sizeof(k1));
+  k1.x = x;
+  k1.out = out;
+  k1.stats = reinterpret_cast<double*>(ws + P.off_stats);
+  k1.attn = attn;
+  k1.attn_mm = reinterpret_cast<float*>(ws + P.off_mm);
+  k1.perc = w->perception;
+  k1.w1 = w->w1;
+  k1.b1 = w->b1;
+  k1.w2 = w->w2;
+  k1.wm = w->wm;
+  k1.bm = w->bm;
+  k1.offw = P.need_k0 ? reinterpret_cast<float*>(ws + P.off_offw) : nullptr;
+  k1.fire = fire;
+  k1.seed = d->rng_seed;
+  k1.rng_step = d->rng_step;
+  k1.sample_base = d->sample_base;
+  k1.B = d->B; k1.C = d->C; k1.H = d->H; k1.W = d->W;
+  k1.hidden = d->hidden;
+  k1.k = P.graph_on ? P.k : 0;
+  k1.RY = P.RY; k1.RX = P.RX; k1.TH = P.TH; k1.TW = P.TW;
+  k1.tiles_x = P.tiles_x; k1.tps = P.tps; k1.total_tiles = P.total_tiles;
+  k1.fire_mode = d->fire_mode;
+  k1.fire_rate = d->fire_rate;
+  k1.alpha_thr = d->alpha_thr;
+  k1.graph_alpha_thr = d->graph_alpha_thr;
+  k1.message_gain = d->message_gain;
+  k1.uniform_w = P.k > 0 ? (float)(1.0 / (double)P.k) : 0.f;
+  k1.flags = d->flags & (GNCA_ZERO_PAD_SHIFT | GNCA_ALIVE_TO_ALIVE | GNCA_HIDDEN_ONLY);
+  if (P.graph_on) {
+    k1.flags |= kGraphOn;
+    if (attn && (d->flags & GNCA_ATTENTION)) k1.flags |= GNCA_ATTENTION;
+  }
+  for (int o = 0; o < 2 * P.k; ++o) k1.offs[o] = d->offsets[o];
+}
+
+static int launch_k0(const gnca_step_desc* d, const gnca_weights* w, const Plan& P, const float* x,
+                     char* ws, hipStream_t st) {
+  K0Args k0;
+  memset(&k0, 0, sizeof(k0));
+  k0.x = x; k0.wq = w->wq; k0.bq = w->bq; k0.wk = w->wk; k0.bk = w->bk; k0.scaling = w->scaling;
+  k0.offw = reinterpret_cast<float*>(ws + P.off_offw);
+  k0.B = d->B; k0.C = d->C; k0.H = d->H; k0.W = d->W; k0.d = d->d_model; k0.k = P.k;
+  for (int o = 0; o < 2 * P.k; ++o) k0.offs[o] = d->offsets[o];
+  const size_t lds = ((size_t)d->C * d->H + d->C + d->d_model + P.k) * sizeof(double);
+  hipLaunchKernelGGL(gnca_k0_offset_weights, dim3(d->B), dim3(kThreads), lds, st, k0);
+  return check_launch();
+}
+
+static int launch_k1(const K1Args& k1, const Plan& P, hipStream_t st) {
+  const int occ = occupancy(P.var->fn, P.lds1);
+  long grid = (long)device_cus() * occ;
+  if (grid > P.total_tiles) grid = P.total_tiles;
+  if (grid < 1) grid = 1;
+  void* args[] = {const_cast<K1Args*>(&k1)};
+  const hipError_t e = hipLaunchKernel(P.var->fn, dim3((unsigned)grid), dim3(kThreads), args, P.lds1, st);
+  if (e != hipSuccess) {
+    g_last_hip = (int)e;
+    return GNCA_ERR_HIP;
+  }
+  return check_launch();
+}
+
+static bool weights_ok(const gnca_step_desc* d, const gnca_weights* w, bool msg_only, const Plan& P) {
+  if (!w) return false;
+  if (!msg_only && (!w->perception || !w->w1 || !w->b1 || !w->w2)) return false;
+  if ((d->flags & GNCA_USE_GROUPNORM) && !msg_only && (!w->gn_weight || !w->gn_bias)) return false;
+  if (P.graph_on && (!w->wm || !w->bm)) return false;
+  if (P.need_k0 && (!w->wq || !w->bq || !w->wk || !w->bk || !w->scaling)) return false;
+  return true;
+}
+
+static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float* x, float* x_out,
+                     const void* fire, float* attn, void* ws, size_t ws_bytes, hipStream_t st,
+                     uint32_t phases = GNCA_PHASE_ALL) {
+  Plan P;
+  if (!make_plan(d, false, &P)) {
+    if (d && d->C >= 4 && d->hidden > 0 && !find_variant(d->C, d->hidden)) return GNCA_ERR_UNSUPPORTED;
+    return GNCA_ERR_INVALID;
+  }
+  if (!x || !x_out || x == x_out || !weights_ok(d, w, false, P)) return GNCA_ERR_INVALID;
+  if ((d->fire_mode == GNCA_FIRE_RAND_F32 || d->fire_mode == GNCA_FIRE_MASK_U8) && !fire)
+    return GNCA_ERR_INVALID;
+  if (d->fire_mode < GNCA_FIRE_NONE || d->fire_mode > GNCA_FIRE_HASH) return GNCA_ERR_INVALID;
+  const bool want_attn = (d->flags & GNCA_GRAPH) && (d->flags & GNCA_ATTENTION);
+  if (want_attn && !attn) return GNCA_ERR_INVALID;
+  if (!ws || ws_bytes < P.ws_bytes) return GNCA_ERR_WORKSPACE;
+  char* wsb = reinterpret_cast<char*>(ws);
+  int rc;
+  if ((phases & GNCA_PHASE_K0) && P.need_k0 && (rc = launch_k0(d, w, P, x, wsb, st)) != GNCA_OK)
+    return rc;
+  // attention with no offsets (k == 0, or radius 1): the reference returns zeros unnormalised
+  if (want_attn && !P.graph_on) {
+    if (hipMemsetAsync(attn, 0, (size_t)d->B * d->H * d->W * sizeof(float), st) != hipSuccess)
+      return GNCA_ERR_HIP;
+  }
+  K1Args k1;
+  float* dx = reinterpret_cast<float*>(wsb + P.off_dx);
+  fill_k1(k1, d, w, P, x, dx, fire, want_attn ? attn : nullptr, wsb);
+  if ((phases & GNCA_PHASE_K1) && (rc = launch_k1(k1, P, st)) != GNCA_OK) return rc;
+  if (!(phases & GNCA_PHASE_K2)) return GNCA_OK;
+  K2Args k2;
+  memset(&k2, 0, sizeof(k2));
+  k2.x = x; k2.dx = dx; k2.out = x_out;
+  k2.stats = reinterpret_cast<const double*>(wsb + P.off_stats);
+  k2.use_gn = (d->flags & GNCA_USE_GROUPNORM) ? 1 : 0;
+  k2.gamma = w->gn_weight; k2.beta = w->gn_bias;
+  k2.attn = (want_attn && P.graph_on) ? attn : nullptr;
+  k2.attn_mm = reinterpret_cast<const float*>(wsb + P.off_mm);
+  k2.B = d->B; k2.C = d->C; k2.H = d->H; k2.W = d->W; k2.tps = P.tps;
+  k2.TH2 = P.TH2; k2.TW2 = P.TW2; k2.tiles2_x = P.tiles2_x; k2.tps2 = P.tps2; k2.total2 = P.total2;
+  k2.gain = d->update_gain; k2.thr = d->alpha_thr; k2.eps = d->gn_eps;
+  hipLaunchKernelGGL(gnca_k2_finalize, dim3(P.total2), dim3(kThreads), P.lds2, st, k2);
+  return check_launch();
+}
+
+}  // namespace gnca
+
+using namespace gnca;
+
+extern "C" {
+
+int gnca_abi_version(void) { return GNCA_ABI_VERSION; }
+
+const char* gnca_status_string(int s) {
+  switch (s) {
+    case GNCA_OK: return "ok";
+    case GNCA_ERR_INVALID: return "invalid argument";
+    case GNCA_ERR_UNSUPPORTED: return "unsupported shape class (C must be <= 32, hidden <= 256)";
+    case GNCA_ERR_WORKSPACE: return "workspace too small";
+    case GNCA_ERR_HIP: return "HIP launch failed";
+    default: return "unknown status";
+  }
+}
+
+int gnca_last_hip_error(void) { return g_last_hip; }
+
+size_t gnca_workspace_bytes(const gnca_step_desc* desc) {
+  Plan P;
+  if (!make_plan(desc, false, &P)) return 0;
+  Plan Q;
+  size_t m = P.ws_bytes;
+  if ((desc->flags & GNCA_GRAPH) && make_plan(desc, true, &Q) && Q.ws_bytes > m) m = Q.ws_bytes;
+  return m;
+}
+
+int gnca_step_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x, float* x_out,
+                  const void* fire, float* attn, void* ws, size_t ws_bytes, void* stream) {
+  return step_impl(desc, w, x, x_out, fire, attn, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream));
+}
+
+int gnca_step_phases_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
+                         float* x_out, const void* fire, float* attn, void* ws, size_t ws_bytes,
+                         void* stream, uint32_t phases) {
+  return step_impl(desc, w, x, x_out, fire, attn, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream),
+                   phases);
+}
+
+int gnca_message_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
+                     float* message, float* attn, void* ws, size_t ws_bytes, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (!desc || !(desc->flags & GNCA_GRAPH)) return GNCA_ERR_INVALID;
+  Plan P;
+  if (!make_plan(desc, true, &P)) return GNCA_ERR_INVALID;
+  if (!x || !message || !weights_ok(desc, w, true, P)) return GNCA_ERR_INVALID;
+  const bool want_attn = (desc->flags & GNCA_ATTENTION) != 0;
+  if (want_attn && !attn) return GNCA_ERR_INVALID;
+  if (!ws || ws_bytes < P.ws_bytes) return GNCA_ERR_WORKSPACE;
+  char* wsb = reinterpret_cast<char*>(ws);
+  const size_t n = (size_t)desc->B * desc->C * desc->H * desc->W;
+  if (!P.graph_on) {  // k == 0: zeros (graph_augmentation.py:141-147)
+    if (hipMemsetAsync(message, 0, n * sizeof(float), st) != hipSuccess) return GNCA_ERR_HIP;
+    if (want_attn &&
+        hipMemsetAsync(attn, 0, (size_t)desc->B * desc->H * desc->W * sizeof(float), st) != hipSuccess)
+      return GNCA_ERR_HIP;
+    return GNCA_OK;
+  }
+  int rc;
+  if (P.need_k0 && (rc = launch_k0(desc, w, P, x, wsb, st)) != GNCA_OK) return rc;
+  K1Args k1;
+  fill_k1(k1, desc, w, P, x, message, nullptr, want_attn ? attn : nullptr, wsb);
+  k1.flags |= kMsgOnly;
+  k1.fire_mode = GNCA_FIRE_NONE;
+  if ((rc = launch_k1(k1, P, st)) != GNCA_OK) return rc;
+  if (want_attn) {
+    dim3 grid((desc->H * desc->W + kThreads - 1) / kThreads, desc->B);
+    if (grid.x > 64) grid.x = 64;
+    hipLaunchKernelGGL(gnca_attn_normalize, grid, dim3(kThreads), 0, st, attn,
+                       reinterpret_cast<const float*>(wsb + P.off_mm), P.tps, desc->H * desc->W);
+    return check_launch();
+  }
+  return GNCA_OK;
+}
+
+int gnca_perceive_f32(int32_t B, int32_t C, int32_t H, int32_t W, const float* weight,
+                      const float* x, float* y, void* stream) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || !weight || !x || !y) return GNCA_ERR_INVALID;
+  const size_t total = (size_t)B * C * H * W;
+  size_t blocks = (total + kThreads - 1) / kThreads;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(gnca_perceive, dim3((unsigned)blocks), dim3(kThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), B, C, H, W, weight, x, y);
+  return check_launch();
+}
+
+int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
+                     const int8_t* offsets, const float* x, float* x_final, float* scratch,
+                     void* ws, size_t ws_bytes, void* stream) {
+  if (!desc || steps < 0 || !x || !x_final || !scratch) return GNCA_ERR_INVALID;
+  if (desc->fire_mode != GNCA_FIRE_NONE && desc->fire_mode != GNCA_FIRE_HASH) return GNCA_ERR_INVALID;
+  if (x == x_final || x == scratch || x_final == scratch) return GNCA_ERR_INVALID;
+  const int k = desc->num_offsets;
+  if ((desc->flags & GNCA_GRAPH) && k > 0 && !offsets) return GNCA_ERR_INVALID;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (steps == 0)
+    return hipMemcpyAsync(x_final, x, (size_t)desc->B * desc->C * desc->H * desc->W * sizeof(float),
+                          hipMemcpyDeviceToDevice, st) == hipSuccess ? GNCA_OK : GNCA_ERR_HIP;
+  gnca_step_desc dt = *desc;
+  dt.flags &= ~GNCA_ATTENTION;
+  const float* src = x;
+  for (int t = 0; t < steps; ++t) {
+    float* dst = ((steps - 1 - t) % 2 == 0) ? x_final : scratch;
+    dt.rng_step = desc->rng_step + t;
+    if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(dt.offsets, offsets + (size_t)t * 2 * k, 2 * k);
+    const int rc = step_impl(&dt, w, src, dst, nullptr, nullptr, ws, ws_bytes, st);
+    if (rc != GNCA_OK) return rc;
+    src = dst;
+  }
+  return GNCA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+"""Shared forward of NeuralCA / NeuralCAGraph: descriptor + weights -> one HIP step."""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .. import _lib as L
+from .. import step as S
+
+
+class _StepFn(torch.autograd.Function):
+    """The HIP step as an autograd node.  Forward values come from libgnca.so.  The BPTT
+    backward kernel is SURVEY.md §8f rank 1 ("next") and is not built yet: asking for a gradient
+    through this node raises instead of silently routing through another implementation."""
+
+    @staticmethod
+    def forward(ctx, x, desc, weights, fire, want_attn, *params):
+        out, attn = S.step(desc, weights, x, fire=fire, want_attention=want_attn)
+        if attn is not None:
+            ctx.mark_non_differentiable(attn)
+        return out, attn
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise NotImplementedError(
+            "graph_neural_cellular_automata_amd: backward through the NCA step (BPTT) is not "
+            "implemented yet; run rollouts under torch.no_grad()")
+
+
+def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen, message_gain,
+             hidden_only: bool, return_attention: bool):
+    x = S.check_state(x, model.n_channels)
+    B, C, H, W = x.shape
+    flags = 0
+    norm = model.norm
+    eps = 1e-3
+    if isinstance(norm, nn.GroupNorm):
+        if norm.num_groups != 1 or not norm.affine:
+            raise ValueError("only GroupNorm(1, C, affine=True) is supported (ncagraph.py:68)")
+        flags |= L.USE_GROUPNORM
+        eps = norm.eps
+    elif not isinstance(norm, nn.Identity):
+        raise ValueError(f"unsupported norm module {type(norm).__name__}")
+    tensors = dict(perception=model.perception.conv.weight, w1=model.update_net[0].weight,
+                   b1=model.update_net[0].bias, w2=model.update_net[2].weight)
+    if flags & L.USE_GROUPNORM:
+        tensors.update(gn_weight=norm.weight, gn_bias=norm.bias)
+    d_model = 1
+    graph_thr = None
+    if graph is not None:
+        flags |= graph.flags(return_attention)
+        if hidden_only:
+            flags |= L.HIDDEN_ONLY
+        tensors.update(graph.weight_tensors())
+        d_model = graph.d_model
+        graph_thr = graph.alpha_thr
+    # stochastic fire mask: the reference's torch.rand draw, on x.device (ncagraph.py:144-146)
+    fire = None
+    fire_mode = L.FIRE_NONE
+    if fire_rate < 1.0:
+        fire = torch.rand(B, 1, H, W, device=x.device)
+        fire_mode = L.FIRE_RAND_F32
+    desc = S.make_desc(B=B, C=C, H=H, W=W, hidden=model.update_net[0].out_channels,
+                       d_model=d_model, offsets=chosen or [], flags=flags,
+                       update_gain=model.update_gain, alpha_thr=model.alpha_thr,
+                       graph_alpha_thr=graph_thr, message_gain=message_gain,
+                       fire_rate=fire_rate, fire_mode=fire_mode, gn_eps=eps)
+    w, keep = S.make_weights(tensors)
+    params = [p for p in model.parameters() if p.requires_grad]
+    if torch.is_grad_enabled() and (x.requires_grad or params):
+        out, attn = _StepFn.apply(x, desc, w, fire, return_attention, *params)
+    else:
+        out, attn = S.step(desc, w, x, fire=fire, want_attention=return_attention)
+    del keep
+    return out, attn

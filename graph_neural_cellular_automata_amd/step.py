@@ -1,0 +1,146 @@
+"""Functional host layer over the C ABI: build descriptors from module state and launch.
+
+Everything here is plumbing around ``libgnca.so``; the arithmetic is in the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _dev_f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"graph_neural_cellular_automata_amd: {name} is on {t.device}; the NCA step runs only "
+            f"on a ROCm GPU (move the model and the state to 'cuda'). There is no CPU path.")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+    return t.contiguous()
+
+
+def check_state(x: torch.Tensor, C: int) -> torch.Tensor:
+    if x.dim() != 4:
+        raise ValueError(f"state must be [B,C,H,W], got {tuple(x.shape)}")
+    if x.shape[1] != C:
+        raise ValueError(f"state has {x.shape[1]} channels, model expects {C}")
+    if C < 4:
+        raise ValueError("the alive mask reads channel 3: n_channels must be >= 4")
+    return _dev_f32(x, "state")
+
+
+def make_desc(*, B, C, H, W, hidden, d_model, offsets, flags, update_gain, alpha_thr,
+              message_gain, fire_rate, fire_mode, gn_eps=1e-3, rng_seed=0, rng_step=0,
+              sample_base=0, graph_alpha_thr=None) -> L.StepDesc:
+    d = L.StepDesc()
+    d.B, d.C, d.H, d.W = int(B), int(C), int(H), int(W)
+    d.hidden, d.d_model = int(hidden), int(d_model)
+    if len(offsets) > L.MAX_OFFSETS:
+        raise ValueError(f"at most {L.MAX_OFFSETS} offsets per step (got {len(offsets)})")
+    d.num_offsets = len(offsets)
+    for o, (dy, dx) in enumerate(offsets):
+        if not (-127 <= dy <= 127 and -127 <= dx <= 127):
+            raise ValueError(f"offset {(dy, dx)} out of int8 range")
+        d.offsets[2 * o] = int(dy)
+        d.offsets[2 * o + 1] = int(dx)
+    d.flags = int(flags)
+    d.update_gain = float(update_gain)
+    d.alpha_thr = float(alpha_thr)
+    d.graph_alpha_thr = float(alpha_thr if graph_alpha_thr is None else graph_alpha_thr)
+    d.message_gain = float(message_gain)
+    d.gn_eps = float(gn_eps)
+    d.fire_rate = float(fire_rate)
+    d.fire_mode = int(fire_mode)
+    d.rng_seed = int(rng_seed) & 0xFFFFFFFFFFFFFFFF
+    d.rng_step = int(rng_step)
+    d.sample_base = int(sample_base)
+    return d
+
+
+def make_weights(tensors: dict) -> tuple[L.Weights, list]:
+    """tensors: name -> device tensor (reference layouts).  Returns the struct and the list of
+    contiguous tensors that must stay alive until the launch is enqueued."""
+    w = L.Weights()
+    keep = []
+    for name, t in tensors.items():
+        if t is None:
+            continue
+        t = _dev_f32(t.detach(), name)
+        keep.append(t)
+        setattr(w, name, t.data_ptr())
+    return w, keep
+
+
+def workspace(desc: L.StepDesc, device) -> torch.Tensor:
+    n = L.load().gnca_workspace_bytes(ctypes.byref(desc))
+    if n == 0:
+        raise L.GncaError(
+            f"unsupported step shape: B={desc.B} C={desc.C} H={desc.H} W={desc.W} "
+            f"hidden={desc.hidden} (compiled for C <= 32, hidden <= 256)")
+    return torch.empty(n, dtype=torch.uint8, device=device)
+
+
+def stream_ptr(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def step(desc, weights, x, fire=None, want_attention=False):
+    """One step: returns (x_out, attn_or_None)."""
+    lib = L.load()
+    x_out = torch.empty_like(x)
+    attn = torch.empty(desc.B, desc.H, desc.W, dtype=torch.float32, device=x.device) \
+        if want_attention else None
+    ws = workspace(desc, x.device)
+    rc = lib.gnca_step_f32(ctypes.byref(desc), ctypes.byref(weights), x.data_ptr(),
+                           x_out.data_ptr(), _ptr(fire), _ptr(attn), ws.data_ptr(), ws.numel(),
+                           stream_ptr(x.device))
+    L.check(rc, "gnca_step_f32")
+    return x_out, attn
+
+
+def message(desc, weights, x, want_attention=False):
+    lib = L.load()
+    m = torch.empty_like(x)
+    attn = torch.empty(desc.B, desc.H, desc.W, dtype=torch.float32, device=x.device) \
+        if want_attention else None
+    ws = workspace(desc, x.device)
+    rc = lib.gnca_message_f32(ctypes.byref(desc), ctypes.byref(weights), x.data_ptr(),
+                              m.data_ptr(), _ptr(attn), ws.data_ptr(), ws.numel(),
+                              stream_ptr(x.device))
+    L.check(rc, "gnca_message_f32")
+    return m, attn
+
+
+def perceive(weight, x):
+    lib = L.load()
+    B, C, H, W = x.shape
+    w = _dev_f32(weight.detach(), "perception weight")
+    y = torch.empty(B, 3 * C, H, W, dtype=torch.float32, device=x.device)
+    rc = lib.gnca_perceive_f32(B, C, H, W, w.data_ptr(), x.data_ptr(), y.data_ptr(),
+                               stream_ptr(x.device))
+    L.check(rc, "gnca_perceive_f32")
+    return y
+
+
+def rollout(desc, weights, x, steps: int, offsets_per_step: list):
+    """``steps`` no-grad steps (GNCA_FIRE_HASH / NONE) in one C call."""
+    lib = L.load()
+    k = desc.num_offsets
+    flat = [v for offs in offsets_per_step for o in offs for v in o]
+    if (desc.flags & L.GRAPH) and k > 0 and len(flat) != steps * 2 * k:
+        raise ValueError("offsets_per_step must hold k pairs for every step")
+    arr = (ctypes.c_int8 * max(1, len(flat)))(*flat) if flat else None
+    out = torch.empty_like(x)
+    scratch = torch.empty_like(x)
+    ws = workspace(desc, x.device)
+    rc = lib.gnca_rollout_f32(ctypes.byref(desc), ctypes.byref(weights), int(steps), arr,
+                              x.data_ptr(), out.data_ptr(), scratch.data_ptr(), ws.data_ptr(),
+                              ws.numel(), stream_ptr(x.device))
+    L.check(rc, "gnca_rollout_f32")
+    return out

@@ -1,0 +1,159 @@
+/*
+ * gnca.h — C ABI of the MI355X-native NCA rollout step (libgnca.so).
+ *
+ * This is the drop-in boundary for ONE hot path of Psylocibe23/Graph_Neural_Cellular_Automata:
+ * the per-cell CA update of NeuralCAGraph.forward / NeuralCA.forward plus the mid-range graph
+ * residual of GraphAugmentation.forward.  The reference has no FFI of its own: its boundary is
+ * the Python nn.Module API, and the Python package graph_neural_cellular_automata_amd mirrors
+ * that API on top of these entry points (ctypes).  INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Every tensor pointer is DEVICE memory, fp32, NCHW contiguous (the reference's layout),
+ *     caller-owned.  Weight pointers use the reference's parameter layouts (Conv2d weights
+ *     [out,in,1,1] / [3C,1,3,3]); no host-side repacking is needed.
+ *   - All work is stream-ordered on `stream`; no entry point synchronises the device, allocates
+ *     memory or copies host<->device, so calls can be captured into a hipGraph.
+ *   - Return value: 0 (GNCA_OK) or a negative gnca_status; gnca_status_string() names it.
+ *   - Stateless and reentrant.
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   gnca_step_f32        NeuralCAGraph.forward        src/modules/ncagraph.py:106-168
+ *                        NeuralCA.forward (graph off) src/modules/nca.py:64-105
+ *                        GraphAugmentation.forward    src/modules/graph_augmentation.py:104-169
+ *                        FixedSobelPerception.forward src/modules/perception.py:21-26
+ *   gnca_message_f32     GraphAugmentation.forward    src/modules/graph_augmentation.py:104-169
+ *   gnca_perceive_f32    FixedSobelPerception.forward src/modules/perception.py:21-26
+ *   gnca_rollout_f32     the rollout loops that call the step once per CA step, e.g.
+ *                        src/training/train_graph_augmented_nca.py:305-321,
+ *                        src/testing/test_graph_augmented_regeneration.py:183-194
+ */
+#ifndef GNCA_H
+#define GNCA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNCA_ABI_VERSION 1
+#define GNCA_MAX_OFFSETS 128   /* >= (2r+1)^2-9 for r <= 5 (112) */
+
+/* gnca_step_desc.flags */
+#define GNCA_GRAPH          (1u << 0)  /* NeuralCAGraph (graph message on); clear = NeuralCA  */
+#define GNCA_USE_GROUPNORM  (1u << 1)  /* nn.GroupNorm(1,C,eps) on dx (ncagraph.py:68)       */
+#define GNCA_HIDDEN_ONLY    (1u << 2)  /* zero message channels 0..3 (ncagraph.py:98-100)     */
+#define GNCA_ALIVE_TO_ALIVE (1u << 3)  /* mask messages by sender alive (graph_aug.py:131)   */
+#define GNCA_ZERO_PAD_SHIFT (1u << 4)  /* _shift2d_pad (dx ignored) instead of torch.roll     */
+#define GNCA_ATTENTION      (1u << 5)  /* also write the normalised attention map [B,H,W]    */
+
+/* gnca_step_desc.fire_mode: the stochastic fire mask of ncagraph.py:144-146 */
+#define GNCA_FIRE_NONE      0  /* fire_rate >= 1: no mask                                   */
+#define GNCA_FIRE_RAND_F32  1  /* fire = (fire[b,0,i,j] <= fire_rate), fire = torch.rand(B,1,H,W) */
+#define GNCA_FIRE_MASK_U8   2  /* fire = (fire[b,0,i,j] != 0), an explicit uint8 mask         */
+#define GNCA_FIRE_HASH      3  /* counter RNG: u(seed, rng_step, sample_base+b, i*W+j) <= fire_rate */
+
+typedef enum gnca_status {
+  GNCA_OK = 0,
+  GNCA_ERR_INVALID = -1,      /* bad shape / argument / null pointer                      */
+  GNCA_ERR_UNSUPPORTED = -2,  /* shape class not compiled in (C > 32, hidden > 256, ...)  */
+  GNCA_ERR_WORKSPACE = -3,    /* workspace too small (see gnca_workspace_bytes)            */
+  GNCA_ERR_HIP = -4           /* a HIP launch failed; gnca_last_hip_error() has the code   */
+} gnca_status;
+
+typedef struct gnca_step_desc {
+  int32_t B, C, H, W;         /* state shape, C >= 4 (alpha is channel 3)                    */
+  int32_t hidden;             /* update_hidden (update_net.0 out channels)                   */
+  int32_t d_model;            /* graph d_model (query/key channels)                          */
+  int32_t num_offsets;        /* k = len(chosen offsets) this step, 0..GNCA_MAX_OFFSETS      */
+  int32_t fire_mode;          /* GNCA_FIRE_*                                                 */
+  uint32_t flags;             /* GNCA_* flag bits                                            */
+  float update_gain;          /* NeuralCAGraph.update_gain                                    */
+  float alpha_thr;            /* NeuralCAGraph.alpha_thr: pre/post-update alive masks         */
+  float graph_alpha_thr;      /* GraphAugmentation.alpha_thr: sender mask (copied at ctor,
+                                 ncagraph.py:79 -> graph_augmentation.py:52,117)              */
+  float message_gain;         /* NeuralCAGraph.message_gain, read per call                    */
+  float gn_eps;               /* GroupNorm eps (1e-3 in the reference)                        */
+  float fire_rate;            /* forward(fire_rate)                                          */
+  uint64_t rng_seed;          /* GNCA_FIRE_HASH only                                          */
+  int64_t rng_step;           /* GNCA_FIRE_HASH only: step index in the rollout               */
+  int64_t sample_base;        /* GNCA_FIRE_HASH only: global index of sample 0 of this shard  */
+  int8_t offsets[2 * GNCA_MAX_OFFSETS]; /* (dy,dx) pairs in random.sample order            */
+} gnca_step_desc;
+
+typedef struct gnca_weights {
+  const float* perception;    /* perception.conv.weight [3C,1,3,3]                          */
+  const float* w1;            /* update_net.0.weight    [hidden,3C,1,1]                     */
+  const float* b1;            /* update_net.0.bias      [hidden]                            */
+  const float* w2;            /* update_net.2.weight    [C,hidden,1,1]                      */
+  const float* gn_weight;     /* norm.weight [C] (NULL if !GNCA_USE_GROUPNORM)              */
+  const float* gn_bias;       /* norm.bias   [C]                                            */
+  const float* wq;            /* graph.query_proj.weight [d,C,1,1]  (graph only)            */
+  const float* bq;            /* graph.query_proj.bias   [d]                                */
+  const float* wk;            /* graph.key_proj.weight   [d,C,1,1]                          */
+  const float* bk;            /* graph.key_proj.bias     [d]                                */
+  const float* wm;            /* graph.msg_proj.weight   [C,C,1,1]                          */
+  const float* bm;            /* graph.msg_proj.bias     [C]                                */
+  const float* scaling;       /* graph.scaling           [] (device scalar)                 */
+} gnca_weights;
+
+/* ABI version (GNCA_ABI_VERSION) — lets a binding check it loaded a matching library. */
+int gnca_abi_version(void);
+
+/* Human-readable name of a gnca_status. */
+const char* gnca_status_string(int status);
+
+/* The hipError_t of the last failed launch on this thread (0 if none). */
+int gnca_last_hip_error(void);
+
+/* Bytes of device workspace gnca_step_f32 needs for `desc` (0 on invalid desc). */
+size_t gnca_workspace_bytes(const gnca_step_desc* desc);
+
+/*
+ * One CA step: x_out = step(x).  Out-of-place (x_out must not alias x), like the reference.
+ *   fire:  NULL, or [B,1,H,W] fp32 uniforms (GNCA_FIRE_RAND_F32) / uint8 mask (GNCA_FIRE_MASK_U8)
+ *   attn:  [B,H,W] fp32, written iff GNCA_ATTENTION (min-max normalised, graph_aug.py:160-167)
+ *   ws:    >= gnca_workspace_bytes(desc) bytes of device memory, 256-B aligned
+ */
+int gnca_step_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
+                  float* x_out, const void* fire, float* attn, void* ws, size_t ws_bytes,
+                  void* stream);
+
+/* Measurement hook: run only the step's kernels named in `phases` (GNCA_PHASE_* bits) with the
+ * same arguments as gnca_step_f32.  gnca_step_f32 == all phases.  Skipping a phase leaves its
+ * outputs stale; bench.py uses this to time K1 alone with HIP events on `stream`. */
+#define GNCA_PHASE_K0 (1u << 0)  /* zero-pad offset weights                */
+#define GNCA_PHASE_K1 (1u << 1)  /* perceive + gather + MLP -> dx, partials */
+#define GNCA_PHASE_K2 (1u << 2)  /* GroupNorm + residual + alive gate       */
+#define GNCA_PHASE_ALL (GNCA_PHASE_K0 | GNCA_PHASE_K1 | GNCA_PHASE_K2)
+int gnca_step_phases_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
+                         float* x_out, const void* fire, float* attn, void* ws, size_t ws_bytes,
+                         void* stream, uint32_t phases);
+
+/*
+ * GraphAugmentation.forward alone: agg_message [B,C,H,W] (before the message policy) and, if
+ * GNCA_ATTENTION, the normalised attention map.  Uses desc's graph fields only.
+ */
+int gnca_message_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
+                     float* message, float* attn, void* ws, size_t ws_bytes, void* stream);
+
+/* FixedSobelPerception.forward: y [B,3C,H,W] in the reference's [id.., sobel_x.., sobel_y..] order. */
+int gnca_perceive_f32(int32_t B, int32_t C, int32_t H, int32_t W, const float* weight,
+                      const float* x, float* y, void* stream);
+
+/*
+ * A whole no-grad rollout of `steps` CA steps with GNCA_FIRE_HASH (or GNCA_FIRE_NONE) masks:
+ * step t uses offsets[t*2*k .. ] (host array, k = desc->num_offsets pairs per step) and
+ * rng_step = desc->rng_step + t.  x is read, x_final receives the last state; scratch holds
+ * one more state ([B,C,H,W] fp32).  Equivalent to `steps` gnca_step_f32 calls.
+ */
+int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
+                     const int8_t* offsets, const float* x, float* x_final, float* scratch,
+                     void* ws, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GNCA_H */

@@ -1,0 +1,64 @@
+"""Run a golden fixture through the C ABI (HIP path) — shared by the GPU parity tests."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from graph_neural_cellular_automata_amd import _lib as L
+from graph_neural_cellular_automata_amd import step as S
+
+WKEYS = dict(perception="perception.conv.weight", w1="update_net.0.weight", b1="update_net.0.bias",
+             w2="update_net.2.weight", gn_weight="norm.weight", gn_bias="norm.bias",
+             wq="graph.query_proj.weight", bq="graph.query_proj.bias", wk="graph.key_proj.weight",
+             bk="graph.key_proj.bias", wm="graph.msg_proj.weight", bm="graph.msg_proj.bias",
+             scaling="graph.scaling")
+
+
+def weights_on(case, dev):
+    ts = {}
+    for k, ref in WKEYS.items():
+        if ref in case.weights:
+            ts[k] = torch.from_numpy(np.ascontiguousarray(case.weights[ref])).float().to(dev)
+    return ts
+
+
+def desc_for(case, B, H, W, chosen, fire_mode, attention=False, **over):
+    m = case.meta
+    flags = 0
+    if m["graph"]:
+        flags |= L.GRAPH
+        if m["alive_to_alive"]:
+            flags |= L.ALIVE_TO_ALIVE
+        if m["zero_padded_shift"]:
+            flags |= L.ZERO_PAD_SHIFT
+        if m["hidden_only"]:
+            flags |= L.HIDDEN_ONLY
+        if attention:
+            flags |= L.ATTENTION
+    if m["use_groupnorm"]:
+        flags |= L.USE_GROUPNORM
+    kw = dict(B=B, C=m["C"], H=H, W=W, hidden=m["Hd"], d_model=m["d"],
+              offsets=chosen if m["graph"] else [], flags=flags, update_gain=m["update_gain"],
+              alpha_thr=m["alpha_thr"], message_gain=m["message_gain"],
+              fire_rate=m["fire_rate"], fire_mode=fire_mode)
+    kw.update(over)
+    return S.make_desc(**kw)
+
+
+def run_case_step(case, dev, t=0, x=None, attention=None):
+    """One step of fixture `case` (its recorded offsets and fire mask) on the GPU."""
+    if x is None:
+        x = torch.from_numpy(case.x_in).to(dev)
+    B, C, H, W = x.shape
+    attention = case.meta["return_attention"] if attention is None else attention
+    fire = None
+    mode = L.FIRE_NONE
+    if case.has("fire_mask"):
+        fire = torch.from_numpy(np.ascontiguousarray(case.fire_mask[t])).to(dev)
+        mode = L.FIRE_MASK_U8
+    desc = desc_for(case, B, H, W, case.chosen(t), mode, attention=attention)
+    w, keep = S.make_weights(weights_on(case, dev))
+    out, attn = S.step(desc, w, x.contiguous(), fire=fire, want_attention=attention and case.meta["graph"])
+    torch.cuda.synchronize()
+    del keep
+    return out, attn

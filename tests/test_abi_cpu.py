@@ -1,0 +1,100 @@
+"""CPU-side checks of the C ABI: the library loads, exports every symbol include/gnca.h declares,
+the ctypes mirrors match the C struct layout, and host-only entry points behave (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from graph_neural_cellular_automata_amd import _lib as L
+from graph_neural_cellular_automata_amd import step as S
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gnca.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(L.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return L.load()
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(gnca_\w+)\s*\(", src, re.M)))
+
+
+def test_exports_every_declared_symbol(lib):
+    names = declared_functions()
+    assert set(names) == set(L.EXPORTS), names
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True).stdout
+    for n in names:
+        assert re.search(rf"\bT {n}$", out, re.M), f"{n} not exported"
+        assert hasattr(lib, n)
+
+
+def test_abi_version(lib):
+    assert lib.gnca_abi_version() == L.ABI_VERSION
+    assert lib.gnca_status_string(0) == b"ok"
+
+
+def test_struct_layout_matches_header(tmp_path):
+    """Compile a C probe against gnca.h and compare offsetof/sizeof with the ctypes mirrors."""
+    fields_d = [f for f, _ in L.StepDesc._fields_]
+    fields_w = [f for f, _ in L.Weights._fields_]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gnca.h"', 'int main(void){']
+    lines.append('printf("desc %zu\\n", sizeof(gnca_step_desc));')
+    lines.append('printf("weights %zu\\n", sizeof(gnca_weights));')
+    for f in fields_d:
+        lines.append(f'printf("d.{f} %zu\\n", offsetof(gnca_step_desc, {f}));')
+    for f in fields_w:
+        lines.append(f'printf("w.{f} %zu\\n", offsetof(gnca_weights, {f}));')
+    lines.append("return 0;}")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True).stdout.splitlines())
+    assert int(got["desc"]) == ctypes.sizeof(L.StepDesc)
+    assert int(got["weights"]) == ctypes.sizeof(L.Weights)
+    for f in fields_d:
+        assert int(got[f"d.{f}"]) == getattr(L.StepDesc, f).offset, f
+    for f in fields_w:
+        assert int(got[f"w.{f}"]) == getattr(L.Weights, f).offset, f
+
+
+def _desc(**kw):
+    base = dict(B=4, C=16, H=72, W=72, hidden=128, d_model=16, offsets=[(2, 3), (-4, 1)],
+                flags=L.GRAPH | L.USE_GROUPNORM | L.ALIVE_TO_ALIVE | L.HIDDEN_ONLY,
+                update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                fire_mode=L.FIRE_HASH)
+    base.update(kw)
+    return S.make_desc(**base)
+
+
+def test_workspace_bytes_host_only(lib):
+    d = _desc()
+    n = lib.gnca_workspace_bytes(ctypes.byref(d))
+    # at least the dx buffer (B*C*H*W fp32)
+    assert n >= 4 * 16 * 72 * 72 * 4
+    d2 = _desc(B=8)
+    assert lib.gnca_workspace_bytes(ctypes.byref(d2)) > n
+
+
+@pytest.mark.parametrize("bad", [dict(C=3), dict(C=36), dict(hidden=512), dict(B=0), dict(H=0)])
+def test_workspace_bytes_rejects_unsupported(lib, bad):
+    d = _desc(**bad)
+    assert lib.gnca_workspace_bytes(ctypes.byref(d)) == 0
+
+
+def test_step_rejects_bad_args_without_touching_gpu(lib):
+    d = _desc()
+    w = L.Weights()
+    # null pointers are rejected before any launch
+    rc = lib.gnca_step_f32(ctypes.byref(d), ctypes.byref(w), None, None, None, None, None, 0, None)
+    assert rc == -1
+    rc = lib.gnca_rollout_f32(ctypes.byref(d), ctypes.byref(w), 3, None, None, None, None, None, 0, None)
+    assert rc == -1

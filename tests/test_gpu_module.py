@@ -1,0 +1,171 @@
+"""GPU tests of the nn.Module surface: the reference's call pattern, RNG contract on device,
+property checks at the benchmark's full size (B=1024 x 16 x 72 x 72)."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nca_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    return torch.device("cuda:0")
+
+
+def _trained_like(dev, zp=False, C=16, seed=0):
+    from graph_neural_cellular_automata_amd import NeuralCAGraph
+    torch.manual_seed(seed)
+    m = NeuralCAGraph(C, 128, update_gain=0.05, alpha_thr=0.12, message_gain=0.25,
+                      graph_zero_padded_shift=zp).to(dev).eval()
+    with torch.no_grad():
+        m.update_net[2].weight.normal_(0, 0.05)
+    return m
+
+
+def _state(B, C, H, W, dev, seed=1):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.rand(B, C, H, W, device=dev, generator=g)
+    x[:, 4:] = torch.randn(B, C - 4, H, W, device=dev, generator=g)
+    return x
+
+
+@pytest.mark.parametrize("zp", [False, True])
+def test_module_forward_rng_contract_and_values(dev, zp):
+    m = _trained_like(dev, zp)
+    x = _state(2, 16, 40, 40, dev)
+    random.seed(5)
+    chosen = random.sample(m.graph.offsets, 8)
+    nxt = random.random()
+    st = torch.cuda.get_rng_state(dev)
+    fire = (torch.rand(2, 1, 40, 40, device=dev) <= 0.6).float()
+    torch.cuda.set_rng_state(st, dev)
+    random.seed(5)
+    with torch.no_grad():
+        out = m(x, fire_rate=0.6)
+    assert random.random() == nxt                       # one random.sample consumed
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    cfg = dict(update_gain=0.05, alpha_thr=0.12, use_groupnorm=True, graph=True,
+               message_gain=0.25, hidden_only=True, zero_padded_shift=zp, alive_to_alive=True)
+    ref = O.nca_step(x.cpu().numpy().astype(np.float64), p, cfg, chosen=chosen,
+                     fire_mask=fire.cpu().numpy().astype(np.float64))
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=2e-6)
+    assert not torch.equal(out, x)
+
+
+def test_torch_rng_consumed_only_when_fire_rate_below_one(dev):
+    m = _trained_like(dev)
+    x = _state(1, 16, 24, 24, dev)
+    st = torch.cuda.get_rng_state(dev)
+    with torch.no_grad():
+        m(x, fire_rate=1.0)
+    assert torch.equal(torch.cuda.get_rng_state(dev), st)
+    with torch.no_grad():
+        m(x, fire_rate=0.5)
+    assert not torch.equal(torch.cuda.get_rng_state(dev), st)
+
+
+def test_attention_and_message_gain_zero(dev):
+    m = _trained_like(dev)
+    x = _state(2, 16, 32, 32, dev)
+    random.seed(3)
+    with torch.no_grad():
+        out, attn = m(x, fire_rate=1.0, return_attention=True)
+    assert attn.shape == (2, 32, 32)
+    assert float(attn.min()) >= 0.0 and float(attn.max()) <= 1.0 + 1e-6
+    # message_gain == 0 (the trainer's "no graph" steps) must equal the classic step
+    from graph_neural_cellular_automata_amd import NeuralCA
+    m.message_gain = 0.0
+    classic = NeuralCA(16, 128, update_gain=0.05, alpha_thr=0.12).to(dev)
+    classic.load_state_dict({k: v for k, v in m.state_dict().items() if not k.startswith("graph.")})
+    with torch.no_grad():
+        a = m(x, fire_rate=1.0)
+        b = classic(x, fire_rate=1.0)
+    assert torch.equal(a, b)
+
+
+def test_full_size_determinism_and_shard_invariance(dev):
+    """B=1024 x 16 x 72 x 72 (the benchmark workload): repeated runs are bitwise identical
+    (no float atomics) and a batch split into shards with the global sample index gives the
+    same states as the whole batch."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    m = _trained_like(dev)
+    B = 1024
+    x = _state(B, 16, 72, 72, dev, seed=7)
+    random.seed(11)
+    offs = [random.sample(m.graph.offsets, 8) for _ in range(3)]
+    tensors = dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
+                   b1=m.update_net[0].bias, w2=m.update_net[2].weight, gn_weight=m.norm.weight,
+                   gn_bias=m.norm.bias, **m.graph.weight_tensors())
+    w, keep = S.make_weights(tensors)
+
+    def roll(xs, base):
+        d = S.make_desc(B=xs.shape[0], C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[0],
+                        flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                        update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                        fire_mode=L.FIRE_HASH, rng_seed=42, sample_base=base)
+        return S.rollout(d, w, xs.contiguous(), 3, offs)
+
+    a = roll(x, 0)
+    b = roll(x, 0)
+    assert torch.equal(a, b)
+    halves = torch.cat([roll(x[:512], 0), roll(x[512:], 512)])
+    assert torch.equal(a, halves)
+    # rollout API == repeated single steps
+    xs = x[:4].contiguous()
+    r = roll(xs, 0)
+    cur = xs
+    for t in range(3):
+        d = S.make_desc(B=4, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[t],
+                        flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                        update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                        fire_mode=L.FIRE_HASH, rng_seed=42, rng_step=t)
+        cur, _ = S.step(d, w, cur)
+    assert torch.equal(r, cur)
+    # the hashed fire mask agrees with the oracle's definition: check one step vs the oracle
+    fm = O.hash_fire_mask(42, 0, 0, 4, 72, 72, 0.5)
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    cfg = dict(update_gain=0.05, alpha_thr=0.12, use_groupnorm=True, graph=True,
+               message_gain=0.25, hidden_only=True, zero_padded_shift=False, alive_to_alive=True)
+    d = S.make_desc(B=4, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[0],
+                    flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                    update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                    fire_mode=L.FIRE_HASH, rng_seed=42, rng_step=0)
+    one, _ = S.step(d, w, xs)
+    ref = O.nca_step(xs.cpu().numpy().astype(np.float64), p, cfg, chosen=offs[0], fire_mask=fm)
+    np.testing.assert_allclose(one.cpu().numpy(), ref, rtol=1e-5, atol=2e-6)
+
+
+def test_long_rollout_drift(dev):
+    """96 steps (the bench's rollout length) against the float64 oracle on the same offsets and
+    hashed masks: |hip - oracle| <= 1e-4 and no alive-mask flips."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    m = _trained_like(dev, seed=3)
+    x = _state(2, 16, 32, 32, dev, seed=9)
+    random.seed(13)
+    T = 96
+    offs = [random.sample(m.graph.offsets, 8) for _ in range(T)]
+    tensors = dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
+                   b1=m.update_net[0].bias, w2=m.update_net[2].weight, gn_weight=m.norm.weight,
+                   gn_bias=m.norm.bias, **m.graph.weight_tensors())
+    w, keep = S.make_weights(tensors)
+    d = S.make_desc(B=2, C=16, H=32, W=32, hidden=128, d_model=16, offsets=offs[0],
+                    flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                    update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                    fire_mode=L.FIRE_HASH, rng_seed=5)
+    got = S.rollout(d, w, x, T, offs).cpu().numpy()
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    cfg = dict(update_gain=0.05, alpha_thr=0.12, use_groupnorm=True, graph=True,
+               message_gain=0.25, hidden_only=True, zero_padded_shift=False, alive_to_alive=True)
+    ref = x.cpu().numpy().astype(np.float64)
+    for t in range(T):
+        ref = O.nca_step(ref, p, cfg, chosen=offs[t], fire_mask=O.hash_fire_mask(5, t, 0, 2, 32, 32, 0.5))
+    assert np.abs(got - ref).max() <= 1e-4
+    np.testing.assert_array_equal(O.alive_mask(got, 0.12), O.alive_mask(ref, 0.12))

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Run GPU steps in order; each under its own time limit.  Test failures (rc 1) continue to the
+# next step; a crash, abort, fault or timeout (any other non-zero rc) ends the session.
+# usage: tools/gpu_session.sh STEP [STEP ...]   STEP in: tests smoke bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    testsall) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps 96 --warmup 8 ;;
+    benchq) run bench 600 python bench.py --steps 24 --warmup 4 --no-cpu ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 24 --warmup 4 --no-cpu ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
