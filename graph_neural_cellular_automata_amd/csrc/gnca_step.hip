@@ -70,7 +70,7 @@ __device__ __forceinline__ float hash_uniform(uint64_t seed, int64_t step, uint6
 // LDS layout of K1 (floats; every region starts on a 16-byte boundary)
 // ------------------------------------------------------------------------------------------
 struct K1Layout {
-  int w1f, w2f, wmf, b1s, bms, percs, wts, red, xs, al, ap, sp, total;
+  int w1f, w2f, wmf, b1s, bms, percs, wts, odl, red, xs, al, ap, sp, total;
   int RH, RW, RWP, PSTR;
 };
 
@@ -98,9 +98,10 @@ __host__ __device__ inline K1Layout k1_layout(int CP, int HDP, int TH, int TW, i
   L.wmf = o; o += MO * 64 * SWM;
   L.b1s = o; o += r4(HDP);
   L.bms = o; o += r4(CP);
-  L.percs = o; o += CP * 28;
+  L.percs = o; o += CP * 36;
   L.wts = o; o += r4(kmax > 0 ? kmax : 1);
-  L.red = o; o += 4 * 8;  // 4 waves x (2 doubles + 2 floats + pad)
+  L.odl = o; o += r4(kmax > 0 ? kmax : 1);
+  L.red = o; o += 16 * 8;  // up to 16 waves x (2 doubles) + 16 x (2 floats)
   L.xs = o; o += CP * L.PSTR;
   L.al = o; o += r4((L.RH + 2) * (L.RW + 2));
   L.ap = o; o += r4(L.RH * L.RW);
@@ -133,7 +134,7 @@ struct K1Args {
 };
 
 template <int CP, int HDP>
-__global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
+__global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CPQ = CP / 4, KS = 3 * CPQ, MT = HDP / 16, MO = (CP + 15) / 16;
   constexpr int KSP = ((((KS + 3) & ~3) >> 2) & 1) ? ((KS + 3) & ~3) : ((KS + 3) & ~3) + 4;
@@ -141,6 +142,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
   constexpr int S2 = ((S2r >> 2) & 1) ? S2r : S2r + 4;
   constexpr int SWMr = (CPQ + 3) & ~3;
   constexpr int SWM = ((SWMr >> 2) & 1) ? SWMr : SWMr + 4;
+  constexpr int NW = kThreads / 64;
 
   const K1Layout L = k1_layout(CP, HDP, a.TH, a.TW, a.RY, a.RX, a.k);
   float* w1f = smem + L.w1f;
@@ -150,6 +152,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
   float* bms = smem + L.bms;
   float* percs = smem + L.percs;
   float* wts = smem + L.wts;
+  int* odl = reinterpret_cast<int*>(smem + L.odl);
   float* red = smem + L.red;
   float* xs = smem + L.xs;
   float* al = smem + L.al;
@@ -158,7 +161,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int C = a.C, H = a.H, W = a.W, Hd = a.hidden;
+  const int C = a.C, H = a.H, W = a.W, Hd = a.hidden, k = a.k;
   const bool msg_only = (a.flags & kMsgOnly) != 0;
   const bool graph_on = (a.flags & kGraphOn) != 0;
   const bool zp = (a.flags & GNCA_ZERO_PAD_SHIFT) != 0;
@@ -166,6 +169,8 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
   const bool want_attn = (a.flags & GNCA_ATTENTION) != 0;
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
+  const int RH = L.RH, RW = L.RW, RWP = L.RWP, PSTR = L.PSTR;
+  const int RY = a.RY, RX = a.RX, TH = a.TH, TW = a.TW;
 
   // ---- weights -> LDS in MFMA fragment order (once per persistent workgroup) ----
   if (!msg_only) {
@@ -186,9 +191,10 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
       w2f[idx] = v;
     }
     for (int idx = tid; idx < HDP; idx += kThreads) b1s[idx] = idx < Hd ? a.b1[idx] : 0.f;
-    for (int idx = tid; idx < CP * 28; idx += kThreads) {
-      const int c = idx / 28, e = idx % 28;
-      percs[idx] = (c < C && e < 27) ? a.perc[(3 * c + e / 9) * 9 + e % 9] : 0.f;
+    // perception weights [c][f][12] (9 taps + 3 zero pads): three 16-B reads per filter
+    for (int idx = tid; idx < CP * 36; idx += kThreads) {
+      const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
+      percs[idx] = (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
     }
   }
   if (graph_on) {
@@ -198,12 +204,19 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
       wmf[idx] = (s < CPQ && co < C && c < C) ? a.wm[co * C + c] : 0.f;
     }
     for (int idx = tid; idx < CP; idx += kThreads) bms[idx] = idx < C ? a.bm[idx] : 0.f;
+    // gather source = cell index - delta in the (RH x RW) region (torus: dy,dx; pad: dy only)
+    for (int o = tid; o < k; o += kThreads)
+      odl[o] = a.offs[2 * o] * RW + (zp ? 0 : a.offs[2 * o + 1]);
   }
 
-  const int RH = L.RH, RW = L.RW, RWP = L.RWP, PSTR = L.PSTR;
-  const int RY = a.RY, RX = a.RX, TH = a.TH, TW = a.TW;
   const int ncell = TH * TW, ngroups = (ncell + 15) >> 4;
   const size_t HW = (size_t)H * W;
+  // staging geometry, fixed for the whole launch: thread -> (column, first row)
+  const int rpp = kThreads / RW;                // x rows per pass
+  const int xvc = tid % RW, xr0 = tid / RW;
+  const int RW2 = RW + 2, RH2 = RH + 2;
+  const int rpp2 = kThreads / RW2;
+  const int avc = tid % RW2, ar0 = tid / RW2;
 
   for (int tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
     const int b = tile / a.tps, tin = tile - b * a.tps;
@@ -212,76 +225,83 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
     const float* xb = a.x + (size_t)b * C * HW;
     __syncthreads();  // previous tile's LDS readers are done
 
-    // ---- stage x region (halo RY x RX), torus-wrapped or zero outside the image ----
-    const int need_x = graph_on ? CP : (msg_only ? 0 : CP);
-    for (int idx = tid; idx < need_x * RH * RW; idx += kThreads) {
-      const int c = idx / (RH * RW), rem = idx - c * RH * RW;
-      const int vr = rem / RW, vc = rem - vr * RW;
-      int ii = i0 - RY + vr, jj = j0 - RX + vc;
-      float v = 0.f;
-      if (c < C) {
-        if (zp) {
-          if (ii >= 0 && ii < H && jj >= 0 && jj < W) v = xb[c * HW + (size_t)ii * W + jj];
-        } else {
-          ii = wrapi(ii, H);
-          jj = wrapi(jj, W);
-          v = xb[c * HW + (size_t)ii * W + jj];
+    // ---- stage x region (halo RY x RX): torus-wrapped, or zero outside the image (pad) ----
+    if (xr0 < rpp) {
+      int jj = j0 - RX + xvc;
+      bool jin = true;
+      if (zp) jin = jj >= 0 && jj < W;
+      else { while (jj < 0) jj += W; while (jj >= W) jj -= W; }
+      for (int vr = xr0; vr < RH; vr += rpp) {
+        int ii = i0 - RY + vr;
+        bool in = jin;
+        if (zp) in = in && ii >= 0 && ii < H;
+        else { while (ii < 0) ii += H; while (ii >= H) ii -= H; }
+        const float* src = xb + (size_t)ii * W + jj;
+        float* dst = xs + vr * RWP + xvc;
+#pragma unroll 4
+        for (int c = 0; c < CP; ++c) {
+          float v = 0.f;
+          if (in && c < C) v = src[c * HW];
+          dst[c * PSTR] = v;
         }
       }
-      xs[c * PSTR + vr * RWP + vc] = v;
     }
     // ---- alpha region (one more ring) ----
-    for (int idx = tid; idx < (RH + 2) * (RW + 2); idx += kThreads) {
-      const int vr = idx / (RW + 2), vc = idx - vr * (RW + 2);
-      int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
-      float v = 0.f;
-      if (zp) {
-        if (ii >= 0 && ii < H && jj >= 0 && jj < W) v = xb[3 * HW + (size_t)ii * W + jj];
-      } else {
-        v = xb[3 * HW + (size_t)wrapi(ii, H) * W + wrapi(jj, W)];
+    if (ar0 < rpp2) {
+      int jj = j0 - RX - 1 + avc;
+      bool jin = true;
+      if (zp) jin = jj >= 0 && jj < W;
+      else { while (jj < 0) jj += W; while (jj >= W) jj -= W; }
+      for (int vr = ar0; vr < RH2; vr += rpp2) {
+        int ii = i0 - RY - 1 + vr;
+        bool in = jin;
+        if (zp) in = in && ii >= 0 && ii < H;
+        else { while (ii < 0) ii += H; while (ii >= H) ii -= H; }
+        al[vr * RW2 + avc] = in ? xb[3 * HW + (size_t)ii * W + jj] : 0.f;
       }
-      al[idx] = v;
     }
     if (graph_on)
-      for (int o = tid; o < a.k; o += kThreads) wts[o] = a.offw ? a.offw[(size_t)b * a.k + o] : a.uniform_w;
+      for (int o = tid; o < k; o += kThreads) wts[o] = a.offw ? a.offw[(size_t)b * k + o] : a.uniform_w;
     __syncthreads();
 
     // ---- alive plane A (max_pool 3x3 > thr, image-bounded, ncagraph.py:85-92) and the
-    //      sender plane (alive_to_alive ? A : 1), zero where the source is off-image (pad) ----
-    for (int idx = tid; idx < RH * RW; idx += kThreads) {
-      const int vr = idx / RW, vc = idx - vr * RW;
+    //      sender plane (alive_to_alive ? A_graph : 1), zero where the source is off-image ----
+    for (int pos = tid; pos < RH * RW; pos += kThreads) {
+      const int vr = pos / RW, vc = pos - vr * RW;
       int iq = i0 - RY + vr, jq = j0 - RX + vc;
       bool in_img = true;
       if (zp) in_img = iq >= 0 && iq < H && jq >= 0 && jq < W;
-      else { iq = wrapi(iq, H); jq = wrapi(jq, W); }
+      else {
+        while (iq < 0) iq += H; while (iq >= H) iq -= H;
+        while (jq < 0) jq += W; while (jq >= W) jq -= W;
+      }
       float A = 0.f, As = 0.f;
       if (in_img) {
-        float mx = -INFINITY;
-        for (int dv = -1; dv <= 1; ++dv) {
-          if (iq + dv < 0 || iq + dv >= H) continue;
-          for (int du = -1; du <= 1; ++du) {
-            if (jq + du < 0 || jq + du >= W) continue;
-            mx = fmaxf(mx, al[(vr + 1 + dv) * (RW + 2) + (vc + 1 + du)]);
-          }
-        }
+        const bool up = iq > 0, dn = iq < H - 1, lf = jq > 0, rt = jq < W - 1;
+        const float* q = al + (vr + 1) * RW2 + (vc + 1);
+        float mx = q[0];
+        if (up) { mx = fmaxf(mx, q[-RW2]); if (lf) mx = fmaxf(mx, q[-RW2 - 1]); if (rt) mx = fmaxf(mx, q[-RW2 + 1]); }
+        if (dn) { mx = fmaxf(mx, q[RW2]); if (lf) mx = fmaxf(mx, q[RW2 - 1]); if (rt) mx = fmaxf(mx, q[RW2 + 1]); }
+        if (lf) mx = fmaxf(mx, q[-1]);
+        if (rt) mx = fmaxf(mx, q[1]);
         A = mx > thr ? 1.f : 0.f;
         As = mx > gthr ? 1.f : 0.f;
       }
-      ap[idx] = A;
-      sp[idx] = a2a ? As : (in_img ? 1.f : 0.f);
+      ap[pos] = A;
+      sp[pos] = a2a ? As : (in_img ? 1.f : 0.f);
     }
     __syncthreads();
 
     double s1 = 0.0, s2 = 0.0;
     float amin = INFINITY, amax = -INFINITY;
 
-    for (int q = wave; q < ngroups; q += kThreads / 64) {
+    for (int q = wave; q < ngroups; q += NW) {
       const int n = 16 * q + c16;
       int ti = n / TW, tj = n - (n / TW) * TW;
       const int i = i0 + ti, j = j0 + tj;
       const bool valid = n < ncell && i < H && j < W;
       if (!valid) { ti = 0; tj = 0; }
-      const int vr = RY + ti, vc = RX + tj;
+      const int pidx = (RY + ti) * RW + (RX + tj);   // cell in the region (RWP == RW)
       const int ic = valid ? i : i0, jc = valid ? j : j0;
 
       // -- graph gather of alive-masked x (linear message: W_M applied after the sum) --
@@ -289,21 +309,18 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
 #pragma unroll
       for (int t = 0; t < CPQ; ++t) gv[t] = 0.f;
       float S = 0.f;
-      if (graph_on) {
-        for (int o = 0; o < a.k; ++o) {
-          const int dy = a.offs[2 * o], dxo = a.offs[2 * o + 1];
-          const int qr = vr - dy, qc = zp ? vc : vc - dxo;
-          const float wsp = wts[o] * sp[qr * RW + qc];
-          S += wsp;
-          const float* xq = xs + g * PSTR + qr * RWP + qc;
-#pragma unroll
-          for (int t = 0; t < CPQ; ++t) gv[t] += wsp * xq[4 * t * PSTR];
-        }
-      }
       f4 accm[MO];
 #pragma unroll
       for (int mo = 0; mo < MO; ++mo) accm[mo] = f4{0.f, 0.f, 0.f, 0.f};
       if (graph_on) {
+        for (int o = 0; o < k; ++o) {
+          const int qi = pidx - odl[o];
+          const float wsp = wts[o] * sp[qi];
+          S += wsp;
+          const float* xq = xs + g * PSTR + qi;
+#pragma unroll
+          for (int t = 0; t < CPQ; ++t) gv[t] = fmaf(wsp, xq[4 * t * PSTR], gv[t]);
+        }
 #pragma unroll
         for (int s = 0; s < CPQ; ++s)
 #pragma unroll
@@ -315,10 +332,9 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
       // -- attention map: sum_o w_o/C * sum_c |A(q) (W_M x(q) + b_M)_c|  (graph_aug.py:160-162) --
       if (want_attn && graph_on) {
         float att = 0.f;
-        for (int o = 0; o < a.k; ++o) {
-          const int dy = a.offs[2 * o], dxo = a.offs[2 * o + 1];
-          const int qr = vr - dy, qc = zp ? vc : vc - dxo;
-          const float* xq = xs + g * PSTR + qr * RWP + qc;
+        for (int o = 0; o < k; ++o) {
+          const int qi = pidx - odl[o];
+          const float* xq = xs + g * PSTR + qi;
           f4 tmp[MO];
 #pragma unroll
           for (int mo = 0; mo < MO; ++mo) tmp[mo] = f4{0.f, 0.f, 0.f, 0.f};
@@ -338,7 +354,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
             }
           part += __shfl_xor(part, 16);
           part += __shfl_xor(part, 32);
-          att += wts[o] * sp[qr * RW + qc] / (float)C * part;
+          att += wts[o] * sp[qi] / (float)C * part;
         }
         if (valid) {
           if (g == 0) a.attn[(size_t)b * HW + (size_t)i * W + j] = att;
@@ -367,7 +383,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
 #pragma unroll
         for (int t = 0; t < CPQ; ++t) {
           const int c = 4 * t + g;
-          const float* xc = xs + c * PSTR + vr * RWP + vc;
+          const float* xc = xs + c * PSTR + pidx;
           float nb[9];
           nb[0] = (up && lf) ? xc[-RWP - 1] : 0.f;
           nb[1] = up ? xc[-RWP] : 0.f;
@@ -378,18 +394,19 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
           nb[6] = (dn && lf) ? xc[RWP - 1] : 0.f;
           nb[7] = dn ? xc[RWP] : 0.f;
           nb[8] = (dn && rt) ? xc[RWP + 1] : 0.f;
-          const f4* pw = reinterpret_cast<const f4*>(percs + c * 28);
-          float wv[28];
-#pragma unroll
-          for (int e = 0; e < 7; ++e) {
-            const f4 q4 = pw[e];
-            wv[4 * e] = q4[0]; wv[4 * e + 1] = q4[1]; wv[4 * e + 2] = q4[2]; wv[4 * e + 3] = q4[3];
-          }
+          const f4* pw = reinterpret_cast<const f4*>(percs + c * 36);
 #pragma unroll
           for (int f = 0; f < 3; ++f) {
-            float acc = 0.f;
-#pragma unroll
-            for (int e = 0; e < 9; ++e) acc = fmaf(wv[9 * f + e], nb[e], acc);
+            const f4 w0 = pw[3 * f], w1 = pw[3 * f + 1], w2 = pw[3 * f + 2];
+            float acc = w0[0] * nb[0];
+            acc = fmaf(w0[1], nb[1], acc);
+            acc = fmaf(w0[2], nb[2], acc);
+            acc = fmaf(w0[3], nb[3], acc);
+            acc = fmaf(w1[0], nb[4], acc);
+            acc = fmaf(w1[1], nb[5], acc);
+            acc = fmaf(w1[2], nb[6], acc);
+            acc = fmaf(w1[3], nb[7], acc);
+            acc = fmaf(w2[0], nb[8], acc);
             y[f * CPQ + t] = acc;
           }
         }
@@ -410,10 +427,14 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
               acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[u], y[s0 + u], acc[m], 0, 0, 0);
         }
       }
-      // -- bias + ReLU, GEMM2: DL = W2 . H  (accumulator rows are GEMM2's B operand) --
-      f4 acc2[MO];
+      // -- bias + ReLU, GEMM2: DL = W2 . H  (accumulator rows are GEMM2's B operand);
+      //    two accumulator chains so dependent MFMAs do not serialise --
+      f4 acc2[2][MO];
 #pragma unroll
-      for (int mo = 0; mo < MO; ++mo) acc2[mo] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int mo = 0; mo < MO; ++mo) {
+        acc2[0][mo] = f4{0.f, 0.f, 0.f, 0.f};
+        acc2[1][mo] = f4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const f4 bb = *reinterpret_cast<const f4*>(b1s + 16 * m + 4 * g);
@@ -426,12 +447,12 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
           const float h = fmaxf(acc[m][r] + bb[r], 0.f);
 #pragma unroll
           for (int mo = 0; mo < MO; ++mo)
-            acc2[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2v[mo][r], h, acc2[mo], 0, 0, 0);
+            acc2[r & 1][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2v[mo][r], h, acc2[r & 1][mo], 0, 0, 0);
         }
       }
 
       // -- masks: stochastic fire (ncagraph.py:144-146), pre-update alive (:149-150) --
-      float keep = ap[vr * RW + vc];
+      float keep = ap[pidx];
       if (a.fire_mode != GNCA_FIRE_NONE) {
         const size_t cell = (size_t)ic * W + jc;
         bool fire;
@@ -450,7 +471,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
         for (int r = 0; r < 4; ++r) {
           const int c = 16 * mo + 4 * g + r;
           if (!valid || c >= C) continue;
-          float v = acc2[mo][r];
+          float v = acc2[0][mo][r] + acc2[1][mo][r];
           if (graph_on && !(hidden_only && c < 4))
             v += tanhf(accm[mo][r] + bms[c] * S) * a.message_gain;
           v = keep != 0.f ? v : 0.f;
@@ -460,7 +481,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
         }
     }
 
-    // ---- per-tile partials: wave shuffle, then across the 4 waves in LDS ----
+    // ---- per-tile partials: wave shuffle, then across the waves in LDS ----
     if (!msg_only) {
       for (int off = 32; off > 0; off >>= 1) {
         s1 += __shfl_xor(s1, off);
@@ -477,22 +498,22 @@ __global__ __launch_bounds__(kThreads) void gnca_k1_update(const K1Args a) {
     if (lane == 0) {
       redd[wave * 2 + 0] = s1;
       redd[wave * 2 + 1] = s2;
-      red[16 + wave * 2 + 0] = amin;
-      red[16 + wave * 2 + 1] = amax;
+      red[4 * NW + wave * 2 + 0] = amin;
+      red[4 * NW + wave * 2 + 1] = amax;
     }
     __syncthreads();
     if (tid == 0) {
       if (!msg_only) {
         double t1 = 0.0, t2 = 0.0;
-        for (int w = 0; w < kThreads / 64; ++w) { t1 += redd[w * 2]; t2 += redd[w * 2 + 1]; }
+        for (int w = 0; w < NW; ++w) { t1 += redd[w * 2]; t2 += redd[w * 2 + 1]; }
         a.stats[(size_t)tile * 2 + 0] = t1;
         a.stats[(size_t)tile * 2 + 1] = t2;
       }
       if (want_attn) {
         float mn = INFINITY, mx = -INFINITY;
-        for (int w = 0; w < kThreads / 64; ++w) {
-          mn = fminf(mn, red[16 + w * 2]);
-          mx = fmaxf(mx, red[16 + w * 2 + 1]);
+        for (int w = 0; w < NW; ++w) {
+          mn = fminf(mn, red[4 * NW + w * 2]);
+          mx = fmaxf(mx, red[4 * NW + w * 2 + 1]);
         }
         a.attn_mm[(size_t)tile * 2 + 0] = mn;
         a.attn_mm[(size_t)tile * 2 + 1] = mx;
