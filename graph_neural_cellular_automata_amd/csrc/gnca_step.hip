@@ -44,8 +44,22 @@ namespace gnca {
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
+
+// Measurement-only ablation switches (tools/ablate.py builds variants with -DGNCA_ABLATE=<bits>;
+// the product library is always built with 0).  Outputs are wrong in an ablated build.
+#ifndef GNCA_ABLATE
+#define GNCA_ABLATE 0
+#endif
+constexpr int kAblStage = 1;     // skip the global->LDS staging loads (LDS keeps old data)
+constexpr int kAblGather = 2;    // skip the offset gather
+constexpr int kAblPerceive = 4;  // skip the 3x3 perception (y = 0)
+constexpr int kAblMfma = 8;      // skip GEMM1/GEMM2 MFMAs
+constexpr int kAblStore = 16;    // skip the dx stores
+constexpr int kAblPlanes = 32;   // skip the alive / sender planes
 constexpr uint32_t kMsgOnly = 1u << 16;   // internal K1 flag: write agg message, skip MLP
 constexpr uint32_t kGraphOn = 1u << 17;   // internal K1 flag: gather + message projection needed
+
+__device__ float g_zero[4];  // LDS-DMA source for off-image cells (zero-initialised)
 
 __device__ __forceinline__ int wrapi(int v, int n) {
   v %= n;
@@ -70,8 +84,8 @@ __device__ __forceinline__ float hash_uniform(uint64_t seed, int64_t step, uint6
 // LDS layout of K1 (floats; every region starts on a 16-byte boundary)
 // ------------------------------------------------------------------------------------------
 struct K1Layout {
-  int w1f, w2f, wmf, b1s, bms, percs, wts, odl, red, xs, al, ap, sp, total;
-  int RH, RW, RWP, PSTR;
+  int b1s, bms, percs, wts, odl, red, wmf, w1f, w2f, sp, ap, xs, total;
+  int RH, RW, PSTR, NI;
 };
 
 __host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
@@ -79,33 +93,38 @@ __host__ __device__ inline int odd4(int v) {  // round up to 4*odd: conflict-fre
   v = r4(v);
   return ((v >> 2) & 1) ? v : v + 4;
 }
+__host__ __device__ constexpr bool w1_in_regs(int CP, int HDP) { return (HDP / 16) * (3 * CP / 4) <= 96; }
 
+// The staged region is the tile plus a (RY+1, RX+1) halo: RY/RX for the gather, +1 for the
+// Sobel taps and the 3x3 alive max-pool of the gather sources.  Each channel plane is filled by
+// NI LDS-DMA wave-instructions of 64 dwords, so its stride PSTR >= 64*NI (and = 16 mod 32).
 __host__ __device__ inline K1Layout k1_layout(int CP, int HDP, int TH, int TW, int RY, int RX,
                                               int kmax) {
   K1Layout L;
   const int CPQ = CP / 4, KS = 3 * CPQ, MT = HDP / 16, MO = (CP + 15) / 16;
   const int KSP = odd4(KS), S2 = odd4(4 * MT), SWM = odd4(CPQ);
-  L.RH = TH + 2 * RY;
-  L.RW = TW + 2 * RX;
-  L.RWP = L.RW;
-  int pstr = L.RH * L.RWP;
-  pstr = (pstr + 31) & ~31;
-  pstr += 16;  // plane stride = 16 (mod 32): lanes 0-15 / 16-31 read different channels
-  L.PSTR = pstr;
+  L.RH = TH + 2 * RY + 2;
+  L.RW = TW + 2 * RX + 2;
+  L.NI = (L.RH * L.RW + 63) / 64;
+  L.PSTR = 64 * L.NI + 16;
+  const int kp = r4(kmax > 0 ? kmax : 4);
   int o = 0;
-  L.w1f = o; o += MT * 64 * KSP;
-  L.w2f = o; o += MO * 64 * S2;
-  L.wmf = o; o += MO * 64 * SWM;
   L.b1s = o; o += r4(HDP);
   L.bms = o; o += r4(CP);
   L.percs = o; o += CP * 36;
-  L.wts = o; o += r4(kmax > 0 ? kmax : 1);
-  L.odl = o; o += r4(kmax > 0 ? kmax : 1);
-  L.red = o; o += 16 * 8;  // up to 16 waves x (2 doubles) + 16 x (2 floats)
-  L.xs = o; o += CP * L.PSTR;
-  L.al = o; o += r4((L.RH + 2) * (L.RW + 2));
-  L.ap = o; o += r4(L.RH * L.RW);
+  L.wts = o; o += kp;
+  L.odl = o; o += kp;
+  L.red = o; o += 32;
+  L.wmf = o; o += MO * 64 * SWM;
+  const int wfrag = MT * 64 * KSP + MO * 64 * S2;
+  const bool alias = w1_in_regs(CP, HDP);   // fragments only needed to fill registers
+  if (!alias) { L.w1f = o; L.w2f = o + MT * 64 * KSP; o += wfrag; }
   L.sp = o; o += r4(L.RH * L.RW);
+  L.ap = o; o += r4(L.RH * L.RW);
+  L.xs = o;
+  int xsz = CP * L.PSTR;
+  if (alias) { L.w1f = o; L.w2f = o + MT * 64 * KSP; if (xsz < wfrag) xsz = wfrag; }
+  o += xsz;
   L.total = o;
   return L;
 }
@@ -143,6 +162,8 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   constexpr int SWMr = (CPQ + 3) & ~3;
   constexpr int SWM = ((SWMr >> 2) & 1) ? SWMr : SWMr + 4;
   constexpr int NW = kThreads / 64;
+  constexpr bool W1REG = w1_in_regs(CP, HDP);
+  constexpr bool W2REG = W1REG && MO * 4 * MT <= 32;
 
   const K1Layout L = k1_layout(CP, HDP, a.TH, a.TW, a.RY, a.RX, a.k);
   float* w1f = smem + L.w1f;
@@ -155,13 +176,12 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   int* odl = reinterpret_cast<int*>(smem + L.odl);
   float* red = smem + L.red;
   float* xs = smem + L.xs;
-  float* al = smem + L.al;
   float* ap = smem + L.ap;
   float* sp = smem + L.sp;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int C = a.C, H = a.H, W = a.W, Hd = a.hidden, k = a.k;
+  const int C = a.C, H = a.H, W = a.W, Hd = a.hidden, k = a.k, kp = (a.k + 3) & ~3;
   const bool msg_only = (a.flags & kMsgOnly) != 0;
   const bool graph_on = (a.flags & kGraphOn) != 0;
   const bool zp = (a.flags & GNCA_ZERO_PAD_SHIFT) != 0;
@@ -169,7 +189,7 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
   const bool want_attn = (a.flags & GNCA_ATTENTION) != 0;
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
-  const int RH = L.RH, RW = L.RW, RWP = L.RWP, PSTR = L.PSTR;
+  const int RH = L.RH, RW = L.RW, RWP = L.RW, PSTR = L.PSTR, NI = L.NI;
   const int RY = a.RY, RX = a.RX, TH = a.TH, TW = a.TW;
 
   // ---- weights -> LDS in MFMA fragment order (once per persistent workgroup) ----
@@ -205,70 +225,95 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
     }
     for (int idx = tid; idx < CP; idx += kThreads) bms[idx] = idx < C ? a.bm[idx] : 0.f;
     // gather source = cell index - delta in the (RH x RW) region (torus: dy,dx; pad: dy only)
-    for (int o = tid; o < k; o += kThreads)
-      odl[o] = a.offs[2 * o] * RW + (zp ? 0 : a.offs[2 * o + 1]);
+    for (int o = tid; o < kp; o += kThreads)
+      odl[o] = o < k ? a.offs[2 * o] * RW + (zp ? 0 : a.offs[2 * o + 1]) : 0;
+  }
+
+  // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch)
+  bool sobel = false;
+  if (!msg_only) {
+    __syncthreads();
+    int ok = 1;
+    for (int idx = tid; idx < C * 27; idx += kThreads) {
+      const int c = idx / 27, e = idx % 27, f = e / 9, tap = e % 9;
+      const int tr = tap / 3, tc = tap % 3;
+      float ref;
+      if (f == 0) ref = (tap == 4) ? 1.f : 0.f;
+      else if (f == 1) ref = (float)((tc == 0 ? 1 : (tc == 2 ? -1 : 0)) * (tr == 1 ? 2 : 1));
+      else ref = (float)((tr == 0 ? 1 : (tr == 2 ? -1 : 0)) * (tc == 1 ? 2 : 1));
+      if (percs[c * 36 + f * 12 + tap] != ref) ok = 0;
+    }
+    sobel = __syncthreads_and(ok) != 0;
+  }
+  // MFMA A-fragments resident in VGPRs when they fit (C <= 16, hidden <= 128)
+  float w1r[W1REG ? MT : 1][W1REG ? KS : 1];
+  float w2r[W2REG ? MO : 1][W2REG ? 4 * MT : 1];
+  if (!msg_only) {
+    __syncthreads();
+    if constexpr (W1REG) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int s0 = 0; s0 < KS; ++s0) w1r[m][s0] = w1f[(m * 64 + lane) * KSP + s0];
+    }
+    if constexpr (W2REG) {
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+        for (int e = 0; e < 4 * MT; ++e) w2r[mo][e] = w2f[(mo * 64 + lane) * S2 + e];
+    }
   }
 
   const int ncell = TH * TW, ngroups = (ncell + 15) >> 4;
   const size_t HW = (size_t)H * W;
-  // staging geometry, fixed for the whole launch: thread -> (column, first row)
-  const int rpp = kThreads / RW;                // x rows per pass
-  const int xvc = tid % RW, xr0 = tid / RW;
-  const int RW2 = RW + 2, RH2 = RH + 2;
-  const int rpp2 = kThreads / RW2;
-  const int avc = tid % RW2, ar0 = tid / RW2;
+  const int RI = RH - 2, RJ = RW - 2;   // inner region (gather sources), ring excluded
 
   for (int tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
     const float* xb = a.x + (size_t)b * C * HW;
-    __syncthreads();  // previous tile's LDS readers are done
+    __syncthreads();  // previous tile's LDS readers are done (and the fragment staging area)
 
-    // ---- stage x region (halo RY x RX): torus-wrapped, or zero outside the image (pad) ----
-    if (xr0 < rpp) {
-      int jj = j0 - RX + xvc;
-      bool jin = true;
-      if (zp) jin = jj >= 0 && jj < W;
-      else { while (jj < 0) jj += W; while (jj >= W) jj -= W; }
-      for (int vr = xr0; vr < RH; vr += rpp) {
-        int ii = i0 - RY + vr;
-        bool in = jin;
-        if (zp) in = in && ii >= 0 && ii < H;
-        else { while (ii < 0) ii += H; while (ii >= H) ii -= H; }
-        const float* src = xb + (size_t)ii * W + jj;
-        float* dst = xs + vr * RWP + xvc;
+    // ---- LDS-DMA staging of the (RH x RW) region of every channel: torus-wrapped, or zero
+    //      (a zero source) outside the image in pad mode.  No VGPR round trip; all in flight. ----
+    if (!(GNCA_ABLATE & kAblStage)) {
+      for (int ii_ = wave; ii_ < NI; ii_ += NW) {
+        const int e = 64 * ii_ + lane;
+        int off = -1;
+        if (e < RH * RW) {
+          const int vr = e / RW, vc = e - (e / RW) * RW;
+          int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
+          if (zp) {
+            if (ii >= 0 && ii < H && jj >= 0 && jj < W) off = ii * W + jj;
+          } else {
+            while (ii < 0) ii += H; while (ii >= H) ii -= H;
+            while (jj < 0) jj += W; while (jj >= W) jj -= W;
+            off = ii * W + jj;
+          }
+        }
+        float* dst = xs + 64 * ii_;
 #pragma unroll 4
         for (int c = 0; c < CP; ++c) {
-          float v = 0.f;
-          if (in && c < C) v = src[c * HW];
-          dst[c * PSTR] = v;
+          const float* src = (off >= 0 && c < C) ? xb + c * HW + off : g_zero;
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)(dst + c * PSTR),
+                                           4, 0, 0);
         }
       }
     }
-    // ---- alpha region (one more ring) ----
-    if (ar0 < rpp2) {
-      int jj = j0 - RX - 1 + avc;
-      bool jin = true;
-      if (zp) jin = jj >= 0 && jj < W;
-      else { while (jj < 0) jj += W; while (jj >= W) jj -= W; }
-      for (int vr = ar0; vr < RH2; vr += rpp2) {
-        int ii = i0 - RY - 1 + vr;
-        bool in = jin;
-        if (zp) in = in && ii >= 0 && ii < H;
-        else { while (ii < 0) ii += H; while (ii >= H) ii -= H; }
-        al[vr * RW2 + avc] = in ? xb[3 * HW + (size_t)ii * W + jj] : 0.f;
-      }
-    }
     if (graph_on)
-      for (int o = tid; o < k; o += kThreads) wts[o] = a.offw ? a.offw[(size_t)b * k + o] : a.uniform_w;
+      for (int o = tid; o < kp; o += kThreads)
+        wts[o] = o >= k ? 0.f : (a.offw ? a.offw[(size_t)b * k + o] : a.uniform_w);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
     // ---- alive plane A (max_pool 3x3 > thr, image-bounded, ncagraph.py:85-92) and the
     //      sender plane (alive_to_alive ? A_graph : 1), zero where the source is off-image ----
-    for (int pos = tid; pos < RH * RW; pos += kThreads) {
-      const int vr = pos / RW, vc = pos - vr * RW;
-      int iq = i0 - RY + vr, jq = j0 - RX + vc;
+    const float* al = xs + 3 * PSTR;   // alpha plane of the region
+    for (int pos = tid; pos < ((GNCA_ABLATE & kAblPlanes) ? 0 : RI * RJ); pos += kThreads) {
+      const int vr = pos / RJ + 1, vc = pos - (pos / RJ) * RJ + 1;
+      int iq = i0 - RY - 1 + vr, jq = j0 - RX - 1 + vc;
       bool in_img = true;
       if (zp) in_img = iq >= 0 && iq < H && jq >= 0 && jq < W;
       else {
@@ -278,17 +323,17 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
       float A = 0.f, As = 0.f;
       if (in_img) {
         const bool up = iq > 0, dn = iq < H - 1, lf = jq > 0, rt = jq < W - 1;
-        const float* q = al + (vr + 1) * RW2 + (vc + 1);
+        const float* q = al + vr * RW + vc;
         float mx = q[0];
-        if (up) { mx = fmaxf(mx, q[-RW2]); if (lf) mx = fmaxf(mx, q[-RW2 - 1]); if (rt) mx = fmaxf(mx, q[-RW2 + 1]); }
-        if (dn) { mx = fmaxf(mx, q[RW2]); if (lf) mx = fmaxf(mx, q[RW2 - 1]); if (rt) mx = fmaxf(mx, q[RW2 + 1]); }
+        if (up) { mx = fmaxf(mx, q[-RW]); if (lf) mx = fmaxf(mx, q[-RW - 1]); if (rt) mx = fmaxf(mx, q[-RW + 1]); }
+        if (dn) { mx = fmaxf(mx, q[RW]); if (lf) mx = fmaxf(mx, q[RW - 1]); if (rt) mx = fmaxf(mx, q[RW + 1]); }
         if (lf) mx = fmaxf(mx, q[-1]);
         if (rt) mx = fmaxf(mx, q[1]);
         A = mx > thr ? 1.f : 0.f;
         As = mx > gthr ? 1.f : 0.f;
       }
-      ap[pos] = A;
-      sp[pos] = a2a ? As : (in_img ? 1.f : 0.f);
+      ap[vr * RW + vc] = A;
+      sp[vr * RW + vc] = a2a ? As : (in_img ? 1.f : 0.f);
     }
     __syncthreads();
 
@@ -301,7 +346,7 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
       const int i = i0 + ti, j = j0 + tj;
       const bool valid = n < ncell && i < H && j < W;
       if (!valid) { ti = 0; tj = 0; }
-      const int pidx = (RY + ti) * RW + (RX + tj);   // cell in the region (RWP == RW)
+      const int pidx = (RY + 1 + ti) * RW + (RX + 1 + tj);   // cell in the staged region
       const int ic = valid ? i : i0, jc = valid ? j : j0;
 
       // -- graph gather of alive-masked x (linear message: W_M applied after the sum) --
@@ -313,13 +358,17 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
 #pragma unroll
       for (int mo = 0; mo < MO; ++mo) accm[mo] = f4{0.f, 0.f, 0.f, 0.f};
       if (graph_on) {
-        for (int o = 0; o < k; ++o) {
-          const int qi = pidx - odl[o];
-          const float wsp = wts[o] * sp[qi];
-          S += wsp;
-          const float* xq = xs + g * PSTR + qi;
+        // k is padded to a multiple of 4 with (weight 0, delta 0) taps: they add 0 * x(p)
+        for (int o0 = 0; o0 < ((GNCA_ABLATE & kAblGather) ? 0 : kp); o0 += 4) {
 #pragma unroll
-          for (int t = 0; t < CPQ; ++t) gv[t] = fmaf(wsp, xq[4 * t * PSTR], gv[t]);
+          for (int u = 0; u < 4; ++u) {
+            const int qi = pidx - odl[o0 + u];
+            const float wsp = wts[o0 + u] * sp[qi];
+            S += wsp;
+            const float* xq = xs + g * PSTR + qi;
+#pragma unroll
+            for (int t = 0; t < CPQ; ++t) gv[t] = fmaf(wsp, xq[4 * t * PSTR], gv[t]);
+          }
         }
 #pragma unroll
         for (int s = 0; s < CPQ; ++s)
@@ -376,7 +425,9 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
         continue;
       }
 
-      // -- perception: 3x3 depthwise cross-correlation, zero padding (perception.py:16-25) --
+      // -- perception: 3x3 depthwise cross-correlation, zero padding (perception.py:16-25).
+      //    All nine taps are read unconditionally (the region has a >= 1 halo) and masked
+      //    with selects at image borders (torus halos hold wrapped values).
       float y[KS];
       {
         const bool up = ic > 0, dn = ic < H - 1, lf = jc > 0, rt = jc < W - 1;
@@ -384,50 +435,56 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
         for (int t = 0; t < CPQ; ++t) {
           const int c = 4 * t + g;
           const float* xc = xs + c * PSTR + pidx;
-          float nb[9];
-          nb[0] = (up && lf) ? xc[-RWP - 1] : 0.f;
-          nb[1] = up ? xc[-RWP] : 0.f;
-          nb[2] = (up && rt) ? xc[-RWP + 1] : 0.f;
-          nb[3] = lf ? xc[-1] : 0.f;
-          nb[4] = xc[0];
-          nb[5] = rt ? xc[1] : 0.f;
-          nb[6] = (dn && lf) ? xc[RWP - 1] : 0.f;
-          nb[7] = dn ? xc[RWP] : 0.f;
-          nb[8] = (dn && rt) ? xc[RWP + 1] : 0.f;
-          const f4* pw = reinterpret_cast<const f4*>(percs + c * 36);
+          float n0 = xc[-RWP - 1], n1 = xc[-RWP], n2 = xc[-RWP + 1];
+          float n3 = xc[-1], n4 = xc[0], n5 = xc[1];
+          float n6 = xc[RWP - 1], n7 = xc[RWP], n8 = xc[RWP + 1];
+          n0 = (up && lf) ? n0 : 0.f; n1 = up ? n1 : 0.f; n2 = (up && rt) ? n2 : 0.f;
+          n3 = lf ? n3 : 0.f;                               n5 = rt ? n5 : 0.f;
+          n6 = (dn && lf) ? n6 : 0.f; n7 = dn ? n7 : 0.f; n8 = (dn && rt) ? n8 : 0.f;
+          if (GNCA_ABLATE & kAblPerceive) {
+            y[t] = 0.f; y[CPQ + t] = 0.f; y[2 * CPQ + t] = 0.f;
+          } else if (sobel) {
+            // identity, Sobel-x [[1,0,-1],[2,0,-2],[1,0,-1]], Sobel-y [[1,2,1],[0,0,0],[-1,-2,-1]]
+            y[t] = n4;
+            y[CPQ + t] = ((n0 + 2.f * n3) + n6) - ((n2 + 2.f * n5) + n8);
+            y[2 * CPQ + t] = ((n0 + 2.f * n1) + n2) - ((n6 + 2.f * n7) + n8);
+          } else {
+            const f4* pw = reinterpret_cast<const f4*>(percs + c * 36);
 #pragma unroll
-          for (int f = 0; f < 3; ++f) {
-            const f4 w0 = pw[3 * f], w1 = pw[3 * f + 1], w2 = pw[3 * f + 2];
-            float acc = w0[0] * nb[0];
-            acc = fmaf(w0[1], nb[1], acc);
-            acc = fmaf(w0[2], nb[2], acc);
-            acc = fmaf(w0[3], nb[3], acc);
-            acc = fmaf(w1[0], nb[4], acc);
-            acc = fmaf(w1[1], nb[5], acc);
-            acc = fmaf(w1[2], nb[6], acc);
-            acc = fmaf(w1[3], nb[7], acc);
-            acc = fmaf(w2[0], nb[8], acc);
-            y[f * CPQ + t] = acc;
+            for (int f = 0; f < 3; ++f) {
+              const f4 w0 = pw[3 * f], w1 = pw[3 * f + 1], w2 = pw[3 * f + 2];
+              float acc = w0[0] * n0;
+              acc = fmaf(w0[1], n1, acc);
+              acc = fmaf(w0[2], n2, acc);
+              acc = fmaf(w0[3], n3, acc);
+              acc = fmaf(w1[0], n4, acc);
+              acc = fmaf(w1[1], n5, acc);
+              acc = fmaf(w1[2], n6, acc);
+              acc = fmaf(w1[3], n7, acc);
+              acc = fmaf(w2[0], n8, acc);
+              y[f * CPQ + t] = acc;
+            }
           }
         }
       }
 
-      // -- GEMM1: H = W1 . Y  (fp32 MFMA, 16 hidden x 16 cells per tile) --
+      // -- GEMM1: H = W1 . Y + b1 (fp32 MFMA, 16 hidden x 16 cells per tile; the bias is the
+      //    accumulator's initial value; k-steps outer, hidden tiles inner: MT independent chains) --
       f4 acc[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int m = 0; m < MT; ++m) acc[m] = *reinterpret_cast<const f4*>(b1s + 16 * m + 4 * g);
 #pragma unroll
-      for (int s0 = 0; s0 < KS; s0 += 4) {
+      for (int s0 = 0; s0 < KS; ++s0) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          const f4 w4 = *reinterpret_cast<const f4*>(w1f + (m * 64 + lane) * KSP + s0);
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (s0 + u < KS)
-              acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[u], y[s0 + u], acc[m], 0, 0, 0);
+          float wa;
+          if constexpr (W1REG) wa = w1r[m][s0];
+          else wa = w1f[(m * 64 + lane) * KSP + s0];
+          if (GNCA_ABLATE & kAblMfma) { asm volatile("" ::"v"(wa), "v"(y[s0])); continue; }
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa, y[s0], acc[m], 0, 0, 0);
         }
       }
-      // -- bias + ReLU, GEMM2: DL = W2 . H  (accumulator rows are GEMM2's B operand);
+      // -- ReLU, GEMM2: DL = W2 . H  (accumulator rows are GEMM2's B operand);
       //    two accumulator chains so dependent MFMAs do not serialise --
       f4 acc2[2][MO];
 #pragma unroll
@@ -435,19 +492,24 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
         acc2[0][mo] = f4{0.f, 0.f, 0.f, 0.f};
         acc2[1][mo] = f4{0.f, 0.f, 0.f, 0.f};
       }
+      // ReLU in place (NaN-preserving like torch.relu; no canonicalising max)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[m][r] = acc[m][r] < 0.f ? 0.f : acc[m][r];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        const f4 bb = *reinterpret_cast<const f4*>(b1s + 16 * m + 4 * g);
-        f4 w2v[MO];
-#pragma unroll
-        for (int mo = 0; mo < MO; ++mo)
-          w2v[mo] = *reinterpret_cast<const f4*>(w2f + (mo * 64 + lane) * S2 + 4 * m);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float h = fmaxf(acc[m][r] + bb[r], 0.f);
+          const float h = acc[m][r];
 #pragma unroll
-          for (int mo = 0; mo < MO; ++mo)
-            acc2[r & 1][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2v[mo][r], h, acc2[r & 1][mo], 0, 0, 0);
+          for (int mo = 0; mo < MO; ++mo) {
+            float wb;
+            if constexpr (W2REG) wb = w2r[mo][4 * m + r];
+            else wb = w2f[(mo * 64 + lane) * S2 + 4 * m + r];
+            if (GNCA_ABLATE & kAblMfma) { asm volatile("" ::"v"(wb), "v"(h)); continue; }
+            acc2[r & 1][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb, h, acc2[r & 1][mo], 0, 0, 0);
+          }
         }
       }
 
@@ -475,7 +537,8 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
           if (graph_on && !(hidden_only && c < 4))
             v += tanhf(accm[mo][r] + bms[c] * S) * a.message_gain;
           v = keep != 0.f ? v : 0.f;
-          a.out[((size_t)b * C + c) * HW + (size_t)i * W + j] = v;
+          if (GNCA_ABLATE & kAblStore) asm volatile("" ::"v"(v));
+          else a.out[((size_t)b * C + c) * HW + (size_t)i * W + j] = v;
           s1 += (double)v;
           s2 += (double)v * (double)v;
         }

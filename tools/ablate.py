@@ -1,0 +1,78 @@
+"""K1 ablation timing (measurement tool, not a test): build libgnca variants with -DGNCA_ABLATE
+bits, then time K1 of each on the bench workload in ONE process, interleaved rounds.
+
+  python tools/ablate.py build            # in the build container (hipcc)
+  python tools/ablate.py run              # on the GPU box
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "build_ablate")
+VARIANTS = {
+    "full": 0, "no_stage": 1, "no_gather": 2, "no_perceive": 4, "no_mfma": 8, "no_store": 16,
+    "no_planes": 32, "mfma_only": 1 | 2 | 4 | 16 | 32, "no_mfma_no_store": 8 | 16,
+    "stage_only": 2 | 4 | 8 | 16 | 32,
+}
+
+
+def build():
+    os.makedirs(OUT, exist_ok=True)
+    src = os.path.join(ROOT, "graph_neural_cellular_automata_amd", "csrc", "gnca_step.hip")
+    procs = []
+    for name, bits in VARIANTS.items():
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               f"-DGNCA_ABLATE={bits}", f"-I{ROOT}/include", src, "-o", os.path.join(OUT, f"lib_{name}.so")]
+        procs.append(subprocess.Popen(cmd, stderr=subprocess.DEVNULL))
+        if len(procs) >= 4:
+            procs.pop(0).wait()
+    for p in procs:
+        p.wait()
+
+
+def run(reps=15, rounds=3):
+    import random
+    import torch
+    import bench
+    from graph_neural_cellular_automata_amd import _lib as L
+    dev = torch.device("cuda:0")
+    libs = {}
+    for name in VARIANTS:
+        lib = ctypes.CDLL(os.path.join(OUT, f"lib_{name}.so"))
+        lib.gnca_step_phases_f32.restype = ctypes.c_int
+        lib.gnca_step_phases_f32.argtypes = [ctypes.POINTER(L.StepDesc), ctypes.POINTER(L.Weights)] + \
+            [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32]
+        lib.gnca_workspace_bytes.restype = ctypes.c_size_t
+        lib.gnca_workspace_bytes.argtypes = [ctypes.POINTER(L.StepDesc)]
+        libs[name] = lib
+    B, H = 1024, 72
+    w, keep = bench.weight_struct(bench.load_weights(dev))
+    x = torch.rand(B, 16, H, H, device=dev)
+    out = torch.empty_like(x)
+    from oracle.nca_oracle import build_offsets
+    d = bench.make_desc(B, H, H, random.Random(0).sample(build_offsets(4), 8), 0)
+    ws = torch.empty(libs["full"].gnca_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream()
+    res = {n: [] for n in libs}
+    for _ in range(rounds):
+        for n, lib in libs.items():
+            for r in range(reps + 2):
+                e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                rc = lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), x.data_ptr(), out.data_ptr(),
+                                              None, None, ws.data_ptr(), ws.numel(), st.cuda_stream, 2)
+                e1.record(st)
+                assert rc == 0, (n, rc)
+                torch.cuda.synchronize()
+                if r >= 2:
+                    res[n].append(e0.elapsed_time(e1))
+    for n, v in res.items():
+        v.sort()
+        print(f"{n:18s} median {v[len(v)//2]:.3f} ms   min {v[0]:.3f} ms")
+
+
+if __name__ == "__main__":
+    build() if sys.argv[1] == "build" else run()
