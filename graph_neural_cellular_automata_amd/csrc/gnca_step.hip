@@ -597,20 +597,22 @@ struct K2Args {
   const float* beta;
   float* attn;           // normalise in place if non-null
   const float* attn_mm;  // [B * tps * 2]
-  int B, C, H, W, tps, TH2, TW2, tiles2_x, tps2, total2;
+  int B, C, H, W, tps, band, nbands;
   float gain, thr, eps;
   int use_gn;
 };
 
+// One workgroup per (sample, band of rows).  LDS: the updated alpha x~_3 over the band + one
+// halo row each side, then the post-update alive mask of the band; the main pass streams
+// (channel, 4-cell) items with 16-byte loads/stores when W % 4 == 0.
 __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float sh_norm[4];
   const int tid = threadIdx.x;
-  const int tile = blockIdx.x;
-  const int b = tile / a.tps2, tin = tile - b * a.tps2;
-  const int ty = tin / a.tiles2_x, tx = tin - ty * a.tiles2_x;
-  const int i0 = ty * a.TH2, j0 = tx * a.TW2;
+  const int b = blockIdx.x / a.nbands, band = blockIdx.x - b * a.nbands;
   const int C = a.C, H = a.H, W = a.W;
+  const int r0 = band * a.band, r1 = min(H, r0 + a.band);
+  const int h0 = max(0, r0 - 1), h1 = min(H, r1 + 1);       // alpha rows incl. halo
   const size_t HW = (size_t)H * W;
 
   if (tid == 0) {
@@ -643,53 +645,93 @@ __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
   const float* xb = a.x + (size_t)b * C * HW;
   const float* db = a.dx + (size_t)b * C * HW;
   float* ob = a.out + (size_t)b * C * HW;
-  const float g3 = a.use_gn ? a.gamma[3] : 1.f, b3 = a.use_gn ? a.beta[3] : 0.f;
+  const bool gn = a.use_gn != 0;
+  const float g3 = gn ? a.gamma[3] : 1.f, b3 = gn ? a.beta[3] : 0.f;
 
-  // updated alpha over the tile + 1-cell ring (-inf off-image: max_pool padding)
-  const int AW = a.TW2 + 2, AH = a.TH2 + 2;
-  float* at = smem;
-  for (int idx = tid; idx < AW * AH; idx += kThreads) {
-    const int r = idx / AW, c = idx - r * AW;
-    const int ii = i0 - 1 + r, jj = j0 - 1 + c;
-    float v = -INFINITY;
-    if (ii >= 0 && ii < H && jj >= 0 && jj < W) {
-      const size_t p = 3 * HW + (size_t)ii * W + jj;
-      float d = db[p];
-      if (a.use_gn) d = (d - mu) * rs * g3 + b3;
-      v = xb[p] + tanhf(d) * a.gain;
+  float* at = smem;                                  // [(h1-h0) x W] updated alpha
+  float* post = smem + (size_t)(a.band + 2) * W;     // [(r1-r0) x W] post-update alive mask
+  const int na = (h1 - h0) * W;
+  for (int e = tid; e < na; e += kThreads) {
+    const size_t p = 3 * HW + (size_t)h0 * W + e;
+    float d = db[p];
+    if (gn) d = (d - mu) * rs * g3 + b3;
+    at[e] = xb[p] + tanhf(d) * a.gain;
+  }
+  __syncthreads();
+  const int nb = (r1 - r0) * W;
+  for (int e = tid; e < nb; e += kThreads) {
+    const int i = r0 + e / W, j = e - (e / W) * W;
+    float mx = -INFINITY;
+    for (int ii = max(0, i - 1); ii <= min(H - 1, i + 1); ++ii) {
+      const float* row = at + (size_t)(ii - h0) * W;
+      mx = fmaxf(mx, row[j]);
+      if (j > 0) mx = fmaxf(mx, row[j - 1]);
+      if (j < W - 1) mx = fmaxf(mx, row[j + 1]);
     }
-    at[idx] = v;
+    post[e] = mx > a.thr ? 1.f : 0.f;
   }
   __syncthreads();
 
-  const int ncell = a.TH2 * a.TW2;
-  for (int n = tid; n < ncell; n += kThreads) {
-    const int ti = n / a.TW2, tj = n - ti * a.TW2;
-    const int i = i0 + ti, j = j0 + tj;
-    if (i >= H || j >= W) continue;
-    const size_t cell = (size_t)i * W + j;
-    float mx = -INFINITY;
+  const size_t base = (size_t)r0 * W;
+  if ((W & 3) == 0) {
+    // a thread owns a 4-cell quad and walks the channels; four channels' loads are issued
+    // together (memory-level parallelism) before their tanh/residual math
+    const int nq = nb >> 2;
+    for (int q = tid; q < nq; q += kThreads) {
+      const size_t cell = base + 4 * (size_t)q;
+      {
+        const f4 al = *reinterpret_cast<const f4*>(at + (r0 - h0) * W + 4 * q);
+        const f4 ps = *reinterpret_cast<const f4*>(post + 4 * q);
+        *reinterpret_cast<f4*>(ob + 3 * HW + cell) = al * ps;
+      }
+      for (int c0 = 0; c0 < C; c0 += 4) {
+        f4 xv[4], dv[4];
 #pragma unroll
-    for (int dv = 0; dv < 3; ++dv)
+        for (int u = 0; u < 4; ++u) {
+          const int c = c0 + u;
+          if (c < C && c != 3) {
+            xv[u] = *reinterpret_cast<const f4*>(xb + c * HW + cell);
+            dv[u] = *reinterpret_cast<const f4*>(db + c * HW + cell);
+          }
+        }
 #pragma unroll
-      for (int du = 0; du < 3; ++du) mx = fmaxf(mx, at[(ti + dv) * AW + tj + du]);
-    const float post = mx > a.thr ? 1.f : 0.f;
-    for (int c = 0; c < C; ++c) {
-      const size_t p = c * HW + cell;
+        for (int u = 0; u < 4; ++u) {
+          const int c = c0 + u;
+          if (c >= C || c == 3) continue;
+          f4 d = dv[u];
+          if (gn) {
+            const float gc = a.gamma[c] * rs, bc = a.beta[c];
+            d = (d - mu) * gc + bc;
+          }
+          f4 v;
+          v[0] = xv[u][0] + tanhf(d[0]) * a.gain;
+          v[1] = xv[u][1] + tanhf(d[1]) * a.gain;
+          v[2] = xv[u][2] + tanhf(d[2]) * a.gain;
+          v[3] = xv[u][3] + tanhf(d[3]) * a.gain;
+          *reinterpret_cast<f4*>(ob + c * HW + cell) = v;
+        }
+      }
+    }
+  } else {
+    for (int it = tid; it < C * nb; it += kThreads) {
+      const int c = it / nb, e = it - c * nb;
+      const size_t p = c * HW + base + e;
       float v;
       if (c == 3) {
-        v = at[(ti + 1) * AW + tj + 1] * post;
+        v = at[(r0 - h0) * W + e] * post[e];
       } else {
         float d = db[p];
-        if (a.use_gn) d = (d - mu) * rs * a.gamma[c] + a.beta[c];
+        if (gn) d = (d - mu) * (a.gamma[c] * rs) + a.beta[c];
         v = xb[p] + tanhf(d) * a.gain;
       }
       ob[p] = v;
     }
-    if (a.attn) {
-      const float amn = sh_norm[2], amx = sh_norm[3];
-      float* ap = a.attn + (size_t)b * HW + cell;
-      *ap = (*ap - amn) / (amx - amn + 1e-8f);
+  }
+  if (a.attn) {
+    const float amn = sh_norm[2], amx = sh_norm[3];
+    for (int e = tid; e < nb; e += kThreads) {
+      float* q = a.attn + (size_t)b * HW + base + e;
+      *q = (*q - amn) / (amx - amn + 1e-8f);
     }
   }
 }
@@ -858,7 +900,7 @@ struct Plan {
   size_t lds1;
   bool graph_on, need_k0;
   // K2
-  int TH2, TW2, tiles2_x, tps2, total2;
+  int band, nbands, total2;
   size_t lds2;
   // workspace carve (bytes)
   size_t off_dx, off_stats, off_mm, off_offw, ws_bytes;
@@ -917,13 +959,19 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->tiles_y = (d->H + bth - 1) / bth;
   P->tps = P->tiles_x * P->tiles_y;
   P->total_tiles = P->tps * d->B;
-  // K2 tiles: full rows up to 128 wide
-  P->TW2 = d->W <= 128 ? d->W : 128;
-  P->TH2 = 8;
-  P->tiles2_x = (d->W + P->TW2 - 1) / P->TW2;
-  P->tps2 = P->tiles2_x * ((d->H + P->TH2 - 1) / P->TH2);
-  P->total2 = P->tps2 * d->B;
-  P->lds2 = (size_t)(P->TH2 + 2) * (P->TW2 + 2) * 4;
+  // K2 bands: ~8 row bands per sample (many small workgroups: no wave-quantisation tail),
+  // each with its alpha rows + 2 halo rows and its post mask in LDS (<= 48 KB)
+  {
+    long rows = (d->H + 7) / 8;
+    const long cap = (48L * 1024 / 4 / d->W - 2) / 2;
+    if (rows > cap) rows = cap;
+    if (rows < 1) rows = 1;
+    P->band = (int)rows;
+    P->nbands = (d->H + P->band - 1) / P->band;
+    P->total2 = P->nbands * d->B;
+    P->lds2 = (size_t)(2 * P->band + 2) * d->W * 4;
+    if (P->lds2 > 64 * 1024) return false;   // W too wide for one row pair
+  }
   // workspace
   size_t o = 0;
   auto carve = [&o](size_t bytes) { size_t at = o; o += (bytes + 255) & ~(size_t)255; return at; };
@@ -1094,7 +1142,7 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   k2.attn = (want_attn && P.graph_on) ? attn : nullptr;
   k2.attn_mm = reinterpret_cast<const float*>(wsb + P.off_mm);
   k2.B = d->B; k2.C = d->C; k2.H = d->H; k2.W = d->W; k2.tps = P.tps;
-  k2.TH2 = P.TH2; k2.TW2 = P.TW2; k2.tiles2_x = P.tiles2_x; k2.tps2 = P.tps2; k2.total2 = P.total2;
+  k2.band = P.band; k2.nbands = P.nbands;
   k2.gain = d->update_gain; k2.thr = d->alpha_thr; k2.eps = d->gn_eps;
   hipLaunchKernelGGL(gnca_k2_finalize, dim3(P.total2), dim3(kThreads), P.lds2, st, k2);
   return check_launch();
