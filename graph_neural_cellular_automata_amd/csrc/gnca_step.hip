@@ -35,6 +35,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 #include "gnca.h"
@@ -84,8 +85,8 @@ __device__ __forceinline__ float hash_uniform(uint64_t seed, int64_t step, uint6
 // LDS layout of K1 (floats; every region starts on a 16-byte boundary)
 // ------------------------------------------------------------------------------------------
 struct K1Layout {
-  int b1s, bms, percs, wts, odl, red, wmf, w1f, w2f, sp, ap, xs, total;
-  int RH, RW, PSTR, NI;
+  int b1s, bms, percs, wts, kp_, red, wmf, w1f, w2f, sp, xs, al, total;
+  int RH, RW, PSTR, NI, NIA, ALW;
 };
 
 __host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
@@ -93,38 +94,39 @@ __host__ __device__ inline int odd4(int v) {  // round up to 4*odd: conflict-fre
   v = r4(v);
   return ((v >> 2) & 1) ? v : v + 4;
 }
-__host__ __device__ constexpr bool w1_in_regs(int CP, int HDP) { return (HDP / 16) * (3 * CP / 4) <= 96; }
+// W1 fragments stay in LDS (read as 16-byte fragments every group: LDS reads cost no VALU, and
+// keeping them out of VGPRs removes spills and leaves room to keep loads in flight)
+__host__ __device__ constexpr bool w1_in_regs(int, int) { return false; }
 
-// The staged region is the tile plus a (RY+1, RX+1) halo: RY/RX for the gather, +1 for the
-// Sobel taps and the 3x3 alive max-pool of the gather sources.  Each channel plane is filled by
-// NI LDS-DMA wave-instructions of 64 dwords, so its stride PSTR >= 64*NI (and = 16 mod 32).
+// The staged region is the tile plus an (RY, RX) halo for the gather (RH x RW per channel, NI
+// LDS-DMA wave-instructions of 64 dwords, plane stride PSTR >= 64*NI and = 16 mod 32), plus one
+// alpha plane with one more ring ((RH+2) x (RW+2), NIA instructions) for the 3x3 alive max-pool of
+// the gather sources and the Sobel-ring cells.
 __host__ __device__ inline K1Layout k1_layout(int CP, int HDP, int TH, int TW, int RY, int RX,
                                               int kmax) {
   K1Layout L;
   const int CPQ = CP / 4, KS = 3 * CPQ, MT = HDP / 16, MO = (CP + 15) / 16;
   const int KSP = odd4(KS), S2 = odd4(4 * MT), SWM = odd4(CPQ);
-  L.RH = TH + 2 * RY + 2;
-  L.RW = TW + 2 * RX + 2;
+  L.RH = TH + 2 * RY;
+  L.RW = TW + 2 * RX;
   L.NI = (L.RH * L.RW + 63) / 64;
   L.PSTR = 64 * L.NI + 16;
+  L.ALW = L.RW + 2;
+  L.NIA = ((L.RH + 2) * L.ALW + 63) / 64;
   const int kp = r4(kmax > 0 ? kmax : 4);
   int o = 0;
   L.b1s = o; o += r4(HDP);
   L.bms = o; o += r4(CP);
   L.percs = o; o += CP * 36;
   L.wts = o; o += kp;
-  L.odl = o; o += kp;
+  L.kp_ = o; o += r4(TH * TW);              // per-tile keep plane (fire, then fire AND alive)
   L.red = o; o += 32;
   L.wmf = o; o += MO * 64 * SWM;
-  const int wfrag = MT * 64 * KSP + MO * 64 * S2;
-  const bool alias = w1_in_regs(CP, HDP);   // fragments only needed to fill registers
-  if (!alias) { L.w1f = o; L.w2f = o + MT * 64 * KSP; o += wfrag; }
+  L.w2f = o; o += MO * 64 * S2;
+  L.w1f = o; o += MT * 64 * KSP;
   L.sp = o; o += r4(L.RH * L.RW);
-  L.ap = o; o += r4(L.RH * L.RW);
-  L.xs = o;
-  int xsz = CP * L.PSTR;
-  if (alias) { L.w1f = o; L.w2f = o + MT * 64 * KSP; if (xsz < wfrag) xsz = wfrag; }
-  o += xsz;
+  L.xs = o; o += CP * L.PSTR;
+  L.al = o; o += 64 * L.NIA;
   L.total = o;
   return L;
 }
@@ -149,10 +151,24 @@ struct K1Args {
   int B, C, H, W, hidden, k, RY, RX, TH, TW, tiles_x, tps, total_tiles, fire_mode;
   float fire_rate, alpha_thr, graph_alpha_thr, message_gain, uniform_w;
   uint32_t flags;
-  int8_t offs[2 * GNCA_MAX_OFFSETS];
+  int odl[GNCA_MAX_OFFSETS];   // gather source delta in the staged region: dy*RW + dx (pad: dy*RW)
 };
 
-template <int CP, int HDP>
+// ReLU with torch.relu's NaN semantics (NaN stays NaN).  Deliberately NOT inline asm: hipcc does
+// not insert the MFMA-result read hazard wait states around an asm statement.
+__device__ __forceinline__ float relu_nan(float v) { return v < 0.f ? 0.f : v; }
+
+// tanh(x) = 1 - 2 / (exp(2x) + 1): v_exp + v_rcp; abs error ~2e-7 (saturates to +-1, NaN-preserving)
+__device__ __forceinline__ float fast_tanh(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // exp(2x)
+  return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+}
+
+// K1.  Template geometry (TH_, TW_, RY_, RX_) and the gather width KU_ are compile-time in the
+// specialised instantiations (every LDS offset becomes an instruction immediate); 0 = runtime.
+// fp32 MFMA shares the SIMD's fp32 datapath with VALU on gfx950 (profiles/r01_ubench_*), so the
+// body is written to minimise VALU instructions per 16-cell group.
+template <int CP, int HDP, int TH_, int TW_, int RY_, int RX_, int KU_>
 __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CPQ = CP / 4, KS = 3 * CPQ, MT = HDP / 16, MO = (CP + 15) / 16;
@@ -163,9 +179,21 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   constexpr int SWM = ((SWMr >> 2) & 1) ? SWMr : SWMr + 4;
   constexpr int NW = kThreads / 64;
   constexpr bool W1REG = w1_in_regs(CP, HDP);
-  constexpr bool W2REG = W1REG && MO * 4 * MT <= 32;
+  constexpr bool W2REG = false;   // W2 fragments are read from LDS right before GEMM2
+  constexpr bool FIXED = TH_ > 0;
+  // compile-time region geometry of the fixed instantiations
+  constexpr int cRH = TH_ + 2 * RY_, cRW = TW_ + 2 * RX_;
+  constexpr int cNI = (cRH * cRW + 63) / 64, cPSTR = 64 * cNI + 16;
+  constexpr int cALW = cRW + 2, cNIA = ((cRH + 2) * cALW + 63) / 64;
+  constexpr int cGPW = (TH_ * TW_ / 16) / NW;   // groups per wave per tile (fixed geometry)
+  static_assert(!FIXED || (TH_ * TW_) % (16 * NW) == 0, "fixed tiles hold whole groups per wave");
 
-  const K1Layout L = k1_layout(CP, HDP, a.TH, a.TW, a.RY, a.RX, a.k);
+  const int TH = FIXED ? TH_ : a.TH, TW = FIXED ? TW_ : a.TW;
+  const int RY = FIXED ? RY_ : a.RY, RX = FIXED ? RX_ : a.RX;
+  const K1Layout L = k1_layout(CP, HDP, TH, TW, RY, RX, a.k);
+  const int RH = FIXED ? cRH : L.RH, RW = FIXED ? cRW : L.RW;
+  const int NI = FIXED ? cNI : L.NI, PSTR = FIXED ? cPSTR : L.PSTR;
+  const int ALW = FIXED ? cALW : L.ALW, NIA = FIXED ? cNIA : L.NIA;
   float* w1f = smem + L.w1f;
   float* w2f = smem + L.w2f;
   float* wmf = smem + L.wmf;
@@ -173,24 +201,25 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   float* bms = smem + L.bms;
   float* percs = smem + L.percs;
   float* wts = smem + L.wts;
-  int* odl = reinterpret_cast<int*>(smem + L.odl);
+  float* fp = smem + L.kp_;      // per-tile keep plane (tile cells)
   float* red = smem + L.red;
   float* xs = smem + L.xs;
-  float* ap = smem + L.ap;
+  float* al = smem + L.al;       // alpha plane with the extra ring
   float* sp = smem + L.sp;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int C = a.C, H = a.H, W = a.W, Hd = a.hidden, k = a.k, kp = (a.k + 3) & ~3;
-  const bool msg_only = (a.flags & kMsgOnly) != 0;
-  const bool graph_on = (a.flags & kGraphOn) != 0;
-  const bool zp = (a.flags & GNCA_ZERO_PAD_SHIFT) != 0;
+  // fixed instantiations: C == CP, torus staging, no message-only / attention, uniform weights
+  const int C = FIXED ? CP : a.C, H = a.H, W = a.W, Hd = a.hidden;
+  const int k = FIXED ? KU_ : a.k, kp = (k + 3) & ~3;
+  const bool msg_only = FIXED ? false : (a.flags & kMsgOnly) != 0;
+  const bool graph_on = FIXED ? (KU_ > 0) : (a.flags & kGraphOn) != 0;
+  const bool zp = FIXED ? false : (a.flags & GNCA_ZERO_PAD_SHIFT) != 0;
   const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
-  const bool want_attn = (a.flags & GNCA_ATTENTION) != 0;
+  const bool want_attn = FIXED ? false : (a.flags & GNCA_ATTENTION) != 0;
+  const bool uniform_w = FIXED ? true : a.offw == nullptr;
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
-  const int RH = L.RH, RW = L.RW, RWP = L.RW, PSTR = L.PSTR, NI = L.NI;
-  const int RY = a.RY, RX = a.RX, TH = a.TH, TW = a.TW;
 
   // ---- weights -> LDS in MFMA fragment order (once per persistent workgroup) ----
   if (!msg_only) {
@@ -211,28 +240,22 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
       w2f[idx] = v;
     }
     for (int idx = tid; idx < HDP; idx += kThreads) b1s[idx] = idx < Hd ? a.b1[idx] : 0.f;
-    // perception weights [c][f][12] (9 taps + 3 zero pads): three 16-B reads per filter
     for (int idx = tid; idx < CP * 36; idx += kThreads) {
       const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
       percs[idx] = (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
     }
   }
-  if (graph_on) {
-    for (int idx = tid; idx < MO * 64 * SWM; idx += kThreads) {
-      const int s = idx % SWM, ml = idx / SWM, l = ml & 63, mo = ml >> 6;
-      const int co = 16 * mo + (l & 15), c = 4 * s + (l >> 4);
-      wmf[idx] = (s < CPQ && co < C && c < C) ? a.wm[co * C + c] : 0.f;
-    }
-    for (int idx = tid; idx < CP; idx += kThreads) bms[idx] = idx < C ? a.bm[idx] : 0.f;
-    // gather source = cell index - delta in the (RH x RW) region (torus: dy,dx; pad: dy only)
-    for (int o = tid; o < kp; o += kThreads)
-      odl[o] = o < k ? a.offs[2 * o] * RW + (zp ? 0 : a.offs[2 * o + 1]) : 0;
+  for (int idx = tid; idx < MO * 64 * SWM; idx += kThreads) {
+    const int s = idx % SWM, ml = idx / SWM, l = ml & 63, mo = ml >> 6;
+    const int co = 16 * mo + (l & 15), c = 4 * s + (l >> 4);
+    wmf[idx] = (graph_on && s < CPQ && co < C && c < C) ? a.wm[co * C + c] : 0.f;
   }
+  for (int idx = tid; idx < CP; idx += kThreads) bms[idx] = (graph_on && idx < C) ? a.bm[idx] : 0.f;
+  __syncthreads();
 
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch)
   bool sobel = false;
   if (!msg_only) {
-    __syncthreads();
     int ok = 1;
     for (int idx = tid; idx < C * 27; idx += kThreads) {
       const int c = idx / 27, e = idx % 27, f = e / 9, tap = e % 9;
@@ -248,8 +271,10 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   // MFMA A-fragments resident in VGPRs when they fit (C <= 16, hidden <= 128)
   float w1r[W1REG ? MT : 1][W1REG ? KS : 1];
   float w2r[W2REG ? MO : 1][W2REG ? 4 * MT : 1];
+  float wmr[MO][CPQ];
+  float bmr[MO][4];
+  float gainr[MO];
   if (!msg_only) {
-    __syncthreads();
     if constexpr (W1REG) {
 #pragma unroll
       for (int m = 0; m < MT; ++m)
@@ -263,10 +288,18 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
         for (int e = 0; e < 4 * MT; ++e) w2r[mo][e] = w2f[(mo * 64 + lane) * S2 + e];
     }
   }
+#pragma unroll
+  for (int mo = 0; mo < MO; ++mo) {
+#pragma unroll
+    for (int s = 0; s < CPQ; ++s) wmr[mo][s] = wmf[(mo * 64 + lane) * SWM + s];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bmr[mo][r] = bms[16 * mo + 4 * g + r];
+    // hidden_only: message channels 0..3 (mo 0, lane group 0) get gain 0 (ncagraph.py:98-100)
+    gainr[mo] = (graph_on && !(hidden_only && mo == 0 && g == 0)) ? a.message_gain : 0.f;
+  }
 
   const int ncell = TH * TW, ngroups = (ncell + 15) >> 4;
   const size_t HW = (size_t)H * W;
-  const int RI = RH - 2, RJ = RW - 2;   // inner region (gather sources), ring excluded
 
   for (int tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
     const int b = tile / a.tps, tin = tile - b * a.tps;
@@ -275,15 +308,19 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
     const float* xb = a.x + (size_t)b * C * HW;
     __syncthreads();  // previous tile's LDS readers are done (and the fragment staging area)
 
-    // ---- LDS-DMA staging of the (RH x RW) region of every channel: torus-wrapped, or zero
-    //      (a zero source) outside the image in pad mode.  No VGPR round trip; all in flight. ----
+    // ---- LDS-DMA staging: the (RH x RW) region of every channel, then the alpha plane with one
+    //      more ring; torus-wrapped, or a zero source outside the image in pad mode.  No VGPR
+    //      round trip; every load of the tile in flight at once. ----
     if (!(GNCA_ABLATE & kAblStage)) {
-      for (int ii_ = wave; ii_ < NI; ii_ += NW) {
-        const int e = 64 * ii_ + lane;
+#pragma unroll 1
+      for (int ii_ = wave; ii_ < NI + NIA; ii_ += NW) {
+        const bool ring = ii_ >= NI;             // wave-uniform
+        const int e = 64 * (ring ? ii_ - NI : ii_) + lane;
+        const int rw = ring ? ALW : RW, rh = ring ? RH + 2 : RH, r0 = ring ? 1 : 0;
         int off = -1;
-        if (e < RH * RW) {
-          const int vr = e / RW, vc = e - (e / RW) * RW;
-          int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
+        if (e < rh * rw) {
+          const int vr = e / rw, vc = e - (e / rw) * rw;
+          int ii = i0 - RY - r0 + vr, jj = j0 - RX - r0 + vc;
           if (zp) {
             if (ii >= 0 && ii < H && jj >= 0 && jj < W) off = ii * W + jj;
           } else {
@@ -292,98 +329,146 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
             off = ii * W + jj;
           }
         }
-        float* dst = xs + 64 * ii_;
-#pragma unroll 4
-        for (int c = 0; c < CP; ++c) {
-          const float* src = (off >= 0 && c < C) ? xb + c * HW + off : g_zero;
+        const bool ok = off >= 0;
+        if (!ok) off = 0;
+        if (ring) {
+          const float* src = ok ? xb + 3 * HW + off : g_zero;
           __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                           (__attribute__((address_space(3))) void*)(dst + c * PSTR),
+                                           (__attribute__((address_space(3))) void*)(al + 64 * (ii_ - NI)),
                                            4, 0, 0);
+        } else {
+          float* dst = xs + 64 * ii_;
+#pragma unroll 4
+          for (int c = 0; c < CP; ++c) {
+            const float* src = (ok && c < C) ? xb + c * HW + off : g_zero;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(dst + c * PSTR),
+                                             4, 0, 0);
+          }
         }
       }
     }
-    if (graph_on)
+    // ---- per-tile side tables while the DMA is in flight: offset weights, fire plane ----
+    if (graph_on && !uniform_w)
       for (int o = tid; o < kp; o += kThreads)
-        wts[o] = o >= k ? 0.f : (a.offw ? a.offw[(size_t)b * k + o] : a.uniform_w);
+        wts[o] = o >= k ? 0.f : a.offw[(size_t)b * k + o];
+#pragma unroll 1
+    for (int n = tid; n < ncell; n += kThreads) {
+      const int ti = n / TW, tj = n - (n / TW) * TW;
+      const int i = min(i0 + ti, H - 1), j = min(j0 + tj, W - 1);
+      const size_t cell = (size_t)i * W + j;
+      bool fire = true;
+      if (a.fire_mode == GNCA_FIRE_RAND_F32)
+        fire = reinterpret_cast<const float*>(a.fire)[(size_t)b * HW + cell] <= a.fire_rate;
+      else if (a.fire_mode == GNCA_FIRE_MASK_U8)
+        fire = reinterpret_cast<const uint8_t*>(a.fire)[(size_t)b * HW + cell] != 0;
+      else if (a.fire_mode == GNCA_FIRE_HASH)
+        fire = hash_uniform(a.seed, a.rng_step, (uint64_t)(a.sample_base + b), cell) <= a.fire_rate;
+      fp[n] = fire ? 1.f : 0.f;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    // ---- alive plane A (max_pool 3x3 > thr, image-bounded, ncagraph.py:85-92) and the
-    //      sender plane (alive_to_alive ? A_graph : 1), zero where the source is off-image ----
-    const float* al = xs + 3 * PSTR;   // alpha plane of the region
-    for (int pos = tid; pos < ((GNCA_ABLATE & kAblPlanes) ? 0 : RI * RJ); pos += kThreads) {
-      const int vr = pos / RJ + 1, vc = pos - (pos / RJ) * RJ + 1;
-      int iq = i0 - RY - 1 + vr, jq = j0 - RX - 1 + vc;
+    // ---- alive masks (max_pool 3x3 > thr, image-bounded, ncagraph.py:85-92): the sender plane
+    //      (alive_to_alive ? A_graph : 1, zero where the source is off-image) over the region, and
+    //      keep = pre-update alive AND fire for the tile cells ----
+#pragma unroll 1
+    for (int pos = tid; pos < ((GNCA_ABLATE & kAblPlanes) ? 0 : RH * RW); pos += kThreads) {
+      const int vr = pos / RW, vc = pos - (pos / RW) * RW;
+      int iq = i0 - RY + vr, jq = j0 - RX + vc;
       bool in_img = true;
       if (zp) in_img = iq >= 0 && iq < H && jq >= 0 && jq < W;
       else {
         while (iq < 0) iq += H; while (iq >= H) iq -= H;
         while (jq < 0) jq += W; while (jq >= W) jq -= W;
       }
-      float A = 0.f, As = 0.f;
-      if (in_img) {
-        const bool up = iq > 0, dn = iq < H - 1, lf = jq > 0, rt = jq < W - 1;
-        const float* q = al + vr * RW + vc;
-        float mx = q[0];
-        if (up) { mx = fmaxf(mx, q[-RW]); if (lf) mx = fmaxf(mx, q[-RW - 1]); if (rt) mx = fmaxf(mx, q[-RW + 1]); }
-        if (dn) { mx = fmaxf(mx, q[RW]); if (lf) mx = fmaxf(mx, q[RW - 1]); if (rt) mx = fmaxf(mx, q[RW + 1]); }
-        if (lf) mx = fmaxf(mx, q[-1]);
-        if (rt) mx = fmaxf(mx, q[1]);
-        A = mx > thr ? 1.f : 0.f;
-        As = mx > gthr ? 1.f : 0.f;
+      const float* q = al + (vr + 1) * ALW + (vc + 1);
+      const float NEG = -INFINITY;
+      const bool up = iq > 0, dn = iq < H - 1, lf = jq > 0, rt = jq < W - 1;
+      const float u0 = q[-ALW - 1], u1 = q[-ALW], u2 = q[-ALW + 1];
+      const float m0 = q[-1], m1 = q[0], m2 = q[1];
+      const float d0 = q[ALW - 1], d1 = q[ALW], d2 = q[ALW + 1];
+      const float mu_ = fmaxf(fmaxf(lf ? u0 : NEG, u1), rt ? u2 : NEG);
+      const float mm_ = fmaxf(fmaxf(lf ? m0 : NEG, m1), rt ? m2 : NEG);
+      const float md_ = fmaxf(fmaxf(lf ? d0 : NEG, d1), rt ? d2 : NEG);
+      const float mx = fmaxf(fmaxf(up ? mu_ : NEG, mm_), dn ? md_ : NEG);
+      const float As = (in_img && mx > gthr) ? 1.f : 0.f;
+      sp[pos] = a2a ? As : (in_img ? 1.f : 0.f);
+      const int ti = vr - RY, tj = vc - RX;
+      if (ti >= 0 && ti < TH && tj >= 0 && tj < TW) {
+        const int n = ti * TW + tj;
+        fp[n] = (in_img && mx > thr) ? fp[n] : 0.f;
       }
-      ap[vr * RW + vc] = A;
-      sp[vr * RW + vc] = a2a ? As : (in_img ? 1.f : 0.f);
     }
     __syncthreads();
 
-    double s1 = 0.0, s2 = 0.0;
+    float s1 = 0.f, s2 = 0.f;   // per-lane fp32 partials of this tile (<= a few dozen values)
     float amin = INFINITY, amax = -INFINITY;
+    const size_t cell0 = (size_t)i0 * W + j0;
 
-    for (int q = wave; q < ngroups; q += NW) {
+    const int qend = FIXED ? cGPW * NW : ngroups;
+#pragma unroll 1
+    for (int q = wave; q < qend; q += NW) {
       const int n = 16 * q + c16;
       int ti = n / TW, tj = n - (n / TW) * TW;
-      const int i = i0 + ti, j = j0 + tj;
-      const bool valid = n < ncell && i < H && j < W;
-      if (!valid) { ti = 0; tj = 0; }
-      const int pidx = (RY + 1 + ti) * RW + (RX + 1 + tj);   // cell in the staged region
-      const int ic = valid ? i : i0, jc = valid ? j : j0;
+      bool valid = true;
+      if constexpr (!FIXED) {
+        valid = n < ncell && i0 + ti < H && j0 + tj < W;
+        if (!valid) { ti = 0; tj = 0; }
+      }
+      const int pidx = (RY + ti) * RW + (RX + tj);   // cell in the staged region
+      const int relcell = ti * W + tj;                       // cell - cell0 in the image
+      const float* xg = xs + g * PSTR;                       // this lane's channel group
 
       // -- graph gather of alive-masked x (linear message: W_M applied after the sum) --
       float gv[CPQ];
 #pragma unroll
       for (int t = 0; t < CPQ; ++t) gv[t] = 0.f;
       float S = 0.f;
+      if (graph_on && !(GNCA_ABLATE & kAblGather)) {
+        if constexpr (KU_ > 0) {
+          // compile-time width, uniform weight 1/k applied once after the sum (exact for k=8)
+#pragma unroll
+          for (int o = 0; o < KU_; ++o) {
+            const int qb = pidx - a.odl[o];
+            const float s_ = sp[qb];
+            S += s_;
+#pragma unroll
+            for (int t = 0; t < CPQ; ++t) gv[t] = fmaf(s_, xg[qb + 4 * t * PSTR], gv[t]);
+          }
+          const float wu = a.uniform_w;
+#pragma unroll
+          for (int t = 0; t < CPQ; ++t) gv[t] *= wu;
+          S *= wu;
+        } else {
+          for (int o = 0; o < k; ++o) {
+            const int qb = pidx - a.odl[o];
+            const float wsp = (uniform_w ? a.uniform_w : wts[o]) * sp[qb];
+            S += wsp;
+#pragma unroll
+            for (int t = 0; t < CPQ; ++t) gv[t] = fmaf(wsp, xg[qb + 4 * t * PSTR], gv[t]);
+          }
+        }
+      }
       f4 accm[MO];
 #pragma unroll
       for (int mo = 0; mo < MO; ++mo) accm[mo] = f4{0.f, 0.f, 0.f, 0.f};
+      // phase fences: keep the scheduler from hoisting every phase's LDS loads to the top of the
+      // group (that costs ~100 VGPRs and spills)
+      __builtin_amdgcn_sched_barrier(0);
       if (graph_on) {
-        // k is padded to a multiple of 4 with (weight 0, delta 0) taps: they add 0 * x(p)
-        for (int o0 = 0; o0 < ((GNCA_ABLATE & kAblGather) ? 0 : kp); o0 += 4) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int qi = pidx - odl[o0 + u];
-            const float wsp = wts[o0 + u] * sp[qi];
-            S += wsp;
-            const float* xq = xs + g * PSTR + qi;
-#pragma unroll
-            for (int t = 0; t < CPQ; ++t) gv[t] = fmaf(wsp, xq[4 * t * PSTR], gv[t]);
-          }
-        }
 #pragma unroll
         for (int s = 0; s < CPQ; ++s)
 #pragma unroll
           for (int mo = 0; mo < MO; ++mo)
-            accm[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wmf[(mo * 64 + lane) * SWM + s], gv[s],
-                                                            accm[mo], 0, 0, 0);
+            accm[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wmr[mo][s], gv[s], accm[mo], 0, 0, 0);
       }
 
       // -- attention map: sum_o w_o/C * sum_c |A(q) (W_M x(q) + b_M)_c|  (graph_aug.py:160-162) --
       if (want_attn && graph_on) {
         float att = 0.f;
         for (int o = 0; o < k; ++o) {
-          const int qi = pidx - odl[o];
-          const float* xq = xs + g * PSTR + qi;
+          const int qb = pidx - a.odl[o];
           f4 tmp[MO];
 #pragma unroll
           for (int mo = 0; mo < MO; ++mo) tmp[mo] = f4{0.f, 0.f, 0.f, 0.f};
@@ -391,22 +476,22 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
           for (int s = 0; s < CPQ; ++s)
 #pragma unroll
             for (int mo = 0; mo < MO; ++mo)
-              tmp[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wmf[(mo * 64 + lane) * SWM + s],
-                                                             xq[4 * s * PSTR], tmp[mo], 0, 0, 0);
+              tmp[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wmr[mo][s], xg[qb + 4 * s * PSTR],
+                                                             tmp[mo], 0, 0, 0);
           float part = 0.f;
 #pragma unroll
           for (int mo = 0; mo < MO; ++mo)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int c = 16 * mo + 4 * g + r;
-              if (c < C) part += fabsf(tmp[mo][r] + bms[c]);
+              if (c < C) part += fabsf(tmp[mo][r] + bmr[mo][r]);
             }
           part += __shfl_xor(part, 16);
           part += __shfl_xor(part, 32);
-          att += wts[o] * sp[qi] / (float)C * part;
+          att += (uniform_w ? a.uniform_w : wts[o]) * sp[qb] / (float)C * part;
         }
         if (valid) {
-          if (g == 0) a.attn[(size_t)b * HW + (size_t)i * W + j] = att;
+          if (g == 0) a.attn[(size_t)b * HW + cell0 + relcell] = att;
           amin = fminf(amin, att);
           amax = fmaxf(amax, att);
         }
@@ -420,135 +505,126 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
           for (int r = 0; r < 4; ++r) {
             const int c = 16 * mo + 4 * g + r;
             if (valid && c < C)
-              a.out[((size_t)b * C + c) * HW + (size_t)i * W + j] = accm[mo][r] + bms[c] * S;
+              a.out[((size_t)b * C + c) * HW + cell0 + relcell] = fmaf(bmr[mo][r], S, accm[mo][r]);
           }
         continue;
       }
 
       // -- perception: 3x3 depthwise cross-correlation, zero padding (perception.py:16-25).
-      //    All nine taps are read unconditionally (the region has a >= 1 halo) and masked
-      //    with selects at image borders (torus halos hold wrapped values).
+      //    Taps are read unconditionally (the region has a >= 1 halo); image-border groups
+      //    (one uniform branch) mask the taps that fall outside the image. --
       float y[KS];
       {
+        const int ic = i0 + ti, jc = j0 + tj;
         const bool up = ic > 0, dn = ic < H - 1, lf = jc > 0, rt = jc < W - 1;
 #pragma unroll
         for (int t = 0; t < CPQ; ++t) {
-          const int c = 4 * t + g;
-          const float* xc = xs + c * PSTR + pidx;
-          float n0 = xc[-RWP - 1], n1 = xc[-RWP], n2 = xc[-RWP + 1];
+          const float* xc = xg + 4 * t * PSTR + pidx;
+          float n0 = xc[-RW - 1], n1 = xc[-RW], n2 = xc[-RW + 1];
           float n3 = xc[-1], n4 = xc[0], n5 = xc[1];
-          float n6 = xc[RWP - 1], n7 = xc[RWP], n8 = xc[RWP + 1];
+          float n6 = xc[RW - 1], n7 = xc[RW], n8 = xc[RW + 1];
           n0 = (up && lf) ? n0 : 0.f; n1 = up ? n1 : 0.f; n2 = (up && rt) ? n2 : 0.f;
           n3 = lf ? n3 : 0.f;                               n5 = rt ? n5 : 0.f;
           n6 = (dn && lf) ? n6 : 0.f; n7 = dn ? n7 : 0.f; n8 = (dn && rt) ? n8 : 0.f;
-          if (GNCA_ABLATE & kAblPerceive) {
-            y[t] = 0.f; y[CPQ + t] = 0.f; y[2 * CPQ + t] = 0.f;
-          } else if (sobel) {
-            // identity, Sobel-x [[1,0,-1],[2,0,-2],[1,0,-1]], Sobel-y [[1,2,1],[0,0,0],[-1,-2,-1]]
+          if (sobel) {
             y[t] = n4;
-            y[CPQ + t] = ((n0 + 2.f * n3) + n6) - ((n2 + 2.f * n5) + n8);
-            y[2 * CPQ + t] = ((n0 + 2.f * n1) + n2) - ((n6 + 2.f * n7) + n8);
+            y[CPQ + t] = (fmaf(2.f, n3, n0) + n6) - (fmaf(2.f, n5, n2) + n8);
+            y[2 * CPQ + t] = (fmaf(2.f, n1, n0) + n2) - (fmaf(2.f, n7, n6) + n8);
           } else {
+            const int c = 4 * t + g;
             const f4* pw = reinterpret_cast<const f4*>(percs + c * 36);
 #pragma unroll
             for (int f = 0; f < 3; ++f) {
               const f4 w0 = pw[3 * f], w1 = pw[3 * f + 1], w2 = pw[3 * f + 2];
               float acc = w0[0] * n0;
-              acc = fmaf(w0[1], n1, acc);
-              acc = fmaf(w0[2], n2, acc);
-              acc = fmaf(w0[3], n3, acc);
-              acc = fmaf(w1[0], n4, acc);
-              acc = fmaf(w1[1], n5, acc);
-              acc = fmaf(w1[2], n6, acc);
-              acc = fmaf(w1[3], n7, acc);
-              acc = fmaf(w2[0], n8, acc);
+              acc = fmaf(w0[1], n1, acc); acc = fmaf(w0[2], n2, acc); acc = fmaf(w0[3], n3, acc);
+              acc = fmaf(w1[0], n4, acc); acc = fmaf(w1[1], n5, acc); acc = fmaf(w1[2], n6, acc);
+              acc = fmaf(w1[3], n7, acc); acc = fmaf(w2[0], n8, acc);
               y[f * CPQ + t] = acc;
             }
           }
         }
       }
 
-      // -- GEMM1: H = W1 . Y + b1 (fp32 MFMA, 16 hidden x 16 cells per tile; the bias is the
-      //    accumulator's initial value; k-steps outer, hidden tiles inner: MT independent chains) --
+      __builtin_amdgcn_sched_barrier(0);
+      // -- GEMM1: H = W1 . Y + b1 (bias as the accumulator's initial value; k-steps outer,
+      //    hidden tiles inner: MT independent chains) --
       f4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = *reinterpret_cast<const f4*>(b1s + 16 * m + 4 * g);
 #pragma unroll
-      for (int s0 = 0; s0 < KS; ++s0) {
+      for (int s0 = 0; s0 < KS; s0 += 4) {
+        f4 w4[MT];
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          float wa;
-          if constexpr (W1REG) wa = w1r[m][s0];
-          else wa = w1f[(m * 64 + lane) * KSP + s0];
-          if (GNCA_ABLATE & kAblMfma) { asm volatile("" ::"v"(wa), "v"(y[s0])); continue; }
-          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa, y[s0], acc[m], 0, 0, 0);
+          if constexpr (W1REG) w4[m] = f4{w1r[m][s0], w1r[m][s0 + 1], w1r[m][s0 + 2], w1r[m][s0 + 3]};
+          else w4[m] = *reinterpret_cast<const f4*>(w1f + (m * 64 + lane) * KSP + s0);
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            if (s0 + u >= KS) continue;
+            if (GNCA_ABLATE & kAblMfma) { asm volatile("" ::"v"(w4[m][u]), "v"(y[s0 + u])); continue; }
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[m][u], y[s0 + u], acc[m], 0, 0, 0);
+          }
       }
-      // -- ReLU, GEMM2: DL = W2 . H  (accumulator rows are GEMM2's B operand);
+      // -- ReLU, GEMM2: DL = W2 . H (accumulator rows are GEMM2's B operand);
       //    two accumulator chains so dependent MFMAs do not serialise --
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[m][r] = relu_nan(acc[m][r]);
       f4 acc2[2][MO];
 #pragma unroll
       for (int mo = 0; mo < MO; ++mo) {
         acc2[0][mo] = f4{0.f, 0.f, 0.f, 0.f};
         acc2[1][mo] = f4{0.f, 0.f, 0.f, 0.f};
       }
-      // ReLU in place (NaN-preserving like torch.relu; no canonicalising max)
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[m][r] = acc[m][r] < 0.f ? 0.f : acc[m][r];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
+        f4 w2v[MO];
+#pragma unroll
+        for (int mo = 0; mo < MO; ++mo)
+          w2v[mo] = *reinterpret_cast<const f4*>(w2f + (mo * 64 + lane) * S2 + 4 * m);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float h = acc[m][r];
 #pragma unroll
           for (int mo = 0; mo < MO; ++mo) {
             float wb;
             if constexpr (W2REG) wb = w2r[mo][4 * m + r];
-            else wb = w2f[(mo * 64 + lane) * S2 + 4 * m + r];
-            if (GNCA_ABLATE & kAblMfma) { asm volatile("" ::"v"(wb), "v"(h)); continue; }
-            acc2[r & 1][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb, h, acc2[r & 1][mo], 0, 0, 0);
+            else wb = w2v[mo][r];
+            if (GNCA_ABLATE & kAblMfma) { asm volatile("" ::"v"(wb), "v"(acc[m][r])); continue; }
+            acc2[r & 1][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb, acc[m][r], acc2[r & 1][mo], 0, 0, 0);
           }
         }
       }
 
-      // -- masks: stochastic fire (ncagraph.py:144-146), pre-update alive (:149-150) --
-      float keep = ap[pidx];
-      if (a.fire_mode != GNCA_FIRE_NONE) {
-        const size_t cell = (size_t)ic * W + jc;
-        bool fire;
-        if (a.fire_mode == GNCA_FIRE_RAND_F32)
-          fire = reinterpret_cast<const float*>(a.fire)[(size_t)b * HW + cell] <= a.fire_rate;
-        else if (a.fire_mode == GNCA_FIRE_MASK_U8)
-          fire = reinterpret_cast<const uint8_t*>(a.fire)[(size_t)b * HW + cell] != 0;
-        else
-          fire = hash_uniform(a.seed, a.rng_step, (uint64_t)(a.sample_base + b), cell) <= a.fire_rate;
-        if (!fire) keep = 0.f;
-      }
-      // -- epilogue: dx = dl + tanh(m)*message_gain (hidden_only), masked --
+      // -- epilogue: dx = (dl + tanh(m)*message_gain) * keep, keep = pre-alive AND fire --
+      const float keep = fp[valid ? n : 0];
+      float* ob = a.out + ((size_t)b * C + 4 * g) * HW + cell0;
 #pragma unroll
       for (int mo = 0; mo < MO; ++mo)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = 16 * mo + 4 * g + r;
-          if (!valid || c >= C) continue;
           float v = acc2[0][mo][r] + acc2[1][mo][r];
-          if (graph_on && !(hidden_only && c < 4))
-            v += tanhf(accm[mo][r] + bms[c] * S) * a.message_gain;
+          if (graph_on) v = fmaf(fast_tanh(fmaf(bmr[mo][r], S, accm[mo][r])), gainr[mo], v);
           v = keep != 0.f ? v : 0.f;
+          if (!valid || c >= C) continue;
           if (GNCA_ABLATE & kAblStore) asm volatile("" ::"v"(v));
-          else a.out[((size_t)b * C + c) * HW + (size_t)i * W + j] = v;
-          s1 += (double)v;
-          s2 += (double)v * (double)v;
+          else ob[(16 * mo + r) * HW + relcell] = v;
+          s1 += v;
+          s2 = fmaf(v, v, s2);
         }
     }
 
-    // ---- per-tile partials: wave shuffle, then across the waves in LDS ----
+    // ---- per-tile partials: fp64 wave shuffle, then across the waves in LDS ----
+    double d1 = s1, d2 = s2;
     if (!msg_only) {
       for (int off = 32; off > 0; off >>= 1) {
-        s1 += __shfl_xor(s1, off);
-        s2 += __shfl_xor(s2, off);
+        d1 += __shfl_xor(d1, off);
+        d2 += __shfl_xor(d2, off);
       }
     }
     if (want_attn) {
@@ -559,8 +635,8 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
     }
     double* redd = reinterpret_cast<double*>(red);
     if (lane == 0) {
-      redd[wave * 2 + 0] = s1;
-      redd[wave * 2 + 1] = s2;
+      redd[wave * 2 + 0] = d1;
+      redd[wave * 2 + 1] = d2;
       red[4 * NW + wave * 2 + 0] = amin;
       red[4 * NW + wave * 2 + 1] = amax;
     }
@@ -868,29 +944,32 @@ __global__ __launch_bounds__(kThreads) void gnca_perceive(int B, int C, int H, i
 // ------------------------------------------------------------------------------------------
 thread_local int g_last_hip = 0;
 
-typedef void (*k1_fn)(K1Args);
-
 struct Variant {
-  int CP, HDP;
+  int CP, HDP, TH, TW, RY, RX, KU;   // TH == 0: runtime geometry (generic)
   const void* fn;
 };
 
-#define GNCA_VARIANT(cp, hd) {cp, hd, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd>)}
+#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>)}
+#define GNCA_FV(cp, hd, th, tw, ry, rx, ku) \
+  {cp, hd, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, th, tw, ry, rx, ku>)}
 static const Variant kVariants[] = {
-    GNCA_VARIANT(4, 32),   GNCA_VARIANT(4, 64),   GNCA_VARIANT(4, 128),
-    GNCA_VARIANT(8, 32),   GNCA_VARIANT(8, 64),   GNCA_VARIANT(8, 128),
-    GNCA_VARIANT(12, 64),  GNCA_VARIANT(12, 128), GNCA_VARIANT(16, 32),
-    GNCA_VARIANT(16, 64),  GNCA_VARIANT(16, 128), GNCA_VARIANT(16, 256),
-    GNCA_VARIANT(20, 128), GNCA_VARIANT(24, 128), GNCA_VARIANT(28, 128),
-    GNCA_VARIANT(32, 64),  GNCA_VARIANT(32, 128),
+    // compile-time geometry: the benchmark / trainer shapes (16 ch, hidden 128, 8x24 tiles)
+    GNCA_FV(16, 128, 8, 24, 4, 4, 8),   // graph, torus, r <= 4, K = 8
+    GNCA_FV(16, 128, 8, 24, 1, 1, 0),   // classic NCA (no gather)
+    // runtime geometry: every other shape class
+    GNCA_GV(4, 32),   GNCA_GV(4, 64),   GNCA_GV(4, 128),  GNCA_GV(8, 32),   GNCA_GV(8, 64),
+    GNCA_GV(8, 128),  GNCA_GV(12, 64),  GNCA_GV(12, 128), GNCA_GV(16, 32),  GNCA_GV(16, 64),
+    GNCA_GV(16, 128), GNCA_GV(16, 256), GNCA_GV(20, 128), GNCA_GV(24, 128), GNCA_GV(28, 128),
+    GNCA_GV(32, 64),  GNCA_GV(32, 128),
 };
-#undef GNCA_VARIANT
+#undef GNCA_GV
+#undef GNCA_FV
 
 static const Variant* find_variant(int C, int Hd) {
   const int CP = (C + 3) & ~3;
   const Variant* best = nullptr;
   for (const Variant& v : kVariants)
-    if (v.CP == CP && v.HDP >= Hd && (!best || v.HDP < best->HDP)) best = &v;
+    if (v.TH == 0 && v.CP == CP && v.HDP >= Hd && (!best || v.HDP < best->HDP)) best = &v;
   return best;
 }
 
@@ -930,12 +1009,32 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->RY = ry;
   P->RX = rx;
   const int CP = P->var->CP, HDP = P->var->HDP;
+  const bool attn_on = attn && P->graph_on;
+  // a compile-time-geometry instantiation, when the shape allows one
+  for (const Variant& v : kVariants) {
+    if (v.TH == 0 || v.CP != CP || v.HDP != HDP || d->C != CP || msg_only || attn_on) continue;
+    if (d->H % v.TH || d->W % v.TW || ry > v.RY || rx > v.RX) continue;
+    if (v.KU > 0 ? !(P->graph_on && !zp && !P->need_k0 && P->k == v.KU) : P->graph_on) continue;
+    const K1Layout L = k1_layout(CP, HDP, v.TH, v.TW, v.RY, v.RX, P->k);
+    if ((size_t)L.total * 4 > 80 * 1024) continue;
+    P->var = &v;
+    P->RY = v.RY;
+    P->RX = v.RX;
+    ry = v.RY;
+    rx = v.RX;
+    break;
+  }
   // tile choice: fewest padded cells + staged halo, LDS <= 80 KB (2 workgroups / CU) if possible
   static const int ths[] = {4, 8, 12, 16, 24};
   static const int tws[] = {8, 12, 16, 24, 32, 48, 64};
   double best = 1e300;
   int bth = 0, btw = 0;
   size_t blds = 0;
+  if (P->var->TH) {
+    bth = P->var->TH;
+    btw = P->var->TW;
+    blds = (size_t)k1_layout(CP, HDP, bth, btw, ry, rx, P->k).total * 4;
+  }
   for (int pass = 0; pass < 2 && !bth; ++pass) {
     const size_t cap = pass == 0 ? 80 * 1024 : (size_t)max_lds_bytes();
     for (int th : ths)
@@ -951,7 +1050,6 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
         if (cost < best) { best = cost; bth = th; btw = tw; blds = bytes; }
       }
   }
-  if (!bth) return false;
   P->TH = bth;
   P->TW = btw;
   P->lds1 = blds;
@@ -1065,7 +1163,10 @@ static void fill_k1(K1Args& k1, const gnca_step_desc* d, const gnca_weights* w, 
     k1.flags |= kGraphOn;
     if (attn && (d->flags & GNCA_ATTENTION)) k1.flags |= GNCA_ATTENTION;
   }
-  for (int o = 0; o < 2 * P.k; ++o) k1.offs[o] = d->offsets[o];
+  const int RW = P.TW + 2 * P.RX;
+  const bool zp = (d->flags & GNCA_ZERO_PAD_SHIFT) != 0;
+  for (int o = 0; o < P.k; ++o)
+    k1.odl[o] = d->offsets[2 * o] * RW + (zp ? 0 : d->offsets[2 * o + 1]);
 }
 
 static int launch_k0(const gnca_step_desc* d, const gnca_weights* w, const Plan& P, const float* x,
