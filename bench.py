@@ -38,6 +38,18 @@ BYTES_PER_CELL = 2 * C * 4                             # 128 B: read x, write x'
 PEAK_F32_MFMA = 157.3e12                               # MI355X_MICROARCH.md, FP32 matrix
 PEAK_HBM = 8.0e12
 FIXTURE = os.path.join(ROOT, "tests", "golden", "graph_torus_latest_grown_b1_72.npz")
+# per-launch HBM traffic of K1/K2 measured by rocprofv3 PMC counters in separate passes
+# (tools/pmc.sh + tools/pmc_traffic.py); counters cannot be read from inside this process
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def pmc_traffic(kernel):
+    try:
+        import json as _j
+        d = _j.load(open(PMC_TRAFFIC))["kernels"][kernel]
+        return d["traffic_bytes"]
+    except Exception:
+        return None
 
 
 def parse():
@@ -140,7 +152,8 @@ def main():
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
     lib = L.load()
-    from oracle.nca_oracle import build_offsets  # offset table only (row-major list)
+    from graph_neural_cellular_automata_amd.modules.graph_augmentation import GraphAugmentation
+    build_offsets = GraphAugmentation._build_offsets   # row-major (dy, dx) table, graph_aug.py:73-83
 
     B, H = args.batch, args.size
     offsets_table = build_offsets(R)
@@ -159,7 +172,7 @@ def main():
 
     def rollout(n, step0, src, dst):
         flat = []
-        for _ in range(n):
+        for _ in range(n):   # the per-step host draw (graph_augmentation.py:121), timed
             for dy, dx in rr.sample(offsets_table, K):
                 flat += [dy, dx]
         arr = (ctypes.c_int8 * len(flat))(*flat)
@@ -212,11 +225,12 @@ def main():
     k2_bytes = cells * C * 4 * 3                   # read x, dx; write x'
     roof = {"bound": "mfma", "kernel": "gnca_k1_update<16,128>", "achieved": k1_flops / (k1_ms * 1e-3) / 1e12,
             "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
-            "frac": k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA, "traffic": None,
+            "frac": k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA, "traffic": pmc_traffic("K1"),
+            "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, profiles/r01_pmc_traffic.json)",
             "k1_ms": k1_ms, "flop_per_launch": k1_flops}
     roof_k2 = {"bound": "hbm", "kernel": "gnca_k2_finalize", "achieved": k2_bytes / (k2_ms * 1e-3) / 1e9,
                "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": k2_bytes / (k2_ms * 1e-3) / PEAK_HBM,
-               "k2_ms": k2_ms, "bytes_per_launch": k2_bytes}
+               "k2_ms": k2_ms, "bytes_per_launch": k2_bytes, "traffic": pmc_traffic("K2")}
 
     if rank == 0:
         cpu = None
