@@ -115,18 +115,18 @@ __host__ __device__ inline K1Layout k1_layout(int CP, int HDP, int TH, int TW, i
   L.NIA = ((L.RH + 2) * L.ALW + 63) / 64;
   const int kp = r4(kmax > 0 ? kmax : 4);
   int o = 0;
+  L.xs = o; o += CP * L.PSTR;               // first: region reads fit the 16-bit DS offsets
+  L.sp = o; o += r4(L.RH * L.RW);
+  L.al = o; o += 64 * L.NIA;
+  L.kp_ = o; o += r4(TH * TW);              // per-tile keep plane (fire, then fire AND alive)
   L.b1s = o; o += r4(HDP);
   L.bms = o; o += r4(CP);
   L.percs = o; o += CP * 36;
   L.wts = o; o += kp;
-  L.kp_ = o; o += r4(TH * TW);              // per-tile keep plane (fire, then fire AND alive)
   L.red = o; o += 32;
   L.wmf = o; o += MO * 64 * SWM;
   L.w2f = o; o += MO * 64 * S2;
   L.w1f = o; o += MT * 64 * KSP;
-  L.sp = o; o += r4(L.RH * L.RW);
-  L.xs = o; o += CP * L.PSTR;
-  L.al = o; o += 64 * L.NIA;
   L.total = o;
   return L;
 }
@@ -312,40 +312,57 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
     //      more ring; torus-wrapped, or a zero source outside the image in pad mode.  No VGPR
     //      round trip; every load of the tile in flight at once. ----
     if (!(GNCA_ABLATE & kAblStage)) {
+      // channel planes: element e of the (RH x RW) region -> image (i0-RY+vr, j0-RX+vc)
 #pragma unroll 1
-      for (int ii_ = wave; ii_ < NI + NIA; ii_ += NW) {
-        const bool ring = ii_ >= NI;             // wave-uniform
-        const int e = 64 * (ring ? ii_ - NI : ii_) + lane;
-        const int rw = ring ? ALW : RW, rh = ring ? RH + 2 : RH, r0 = ring ? 1 : 0;
-        int off = -1;
-        if (e < rh * rw) {
-          const int vr = e / rw, vc = e - (e / rw) * rw;
-          int ii = i0 - RY - r0 + vr, jj = j0 - RX - r0 + vc;
+      for (int ii_ = wave; ii_ < NI; ii_ += NW) {
+        const int e = 64 * ii_ + lane;
+        int off = 0;          // lanes past the region fill the plane's pad from a valid address
+        bool ok = true;
+        if (e < RH * RW) {
+          const int vr = e / RW, vc = e - (e / RW) * RW;
+          int ii = i0 - RY + vr, jj = j0 - RX + vc;
           if (zp) {
-            if (ii >= 0 && ii < H && jj >= 0 && jj < W) off = ii * W + jj;
+            ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
+            off = ok ? ii * W + jj : 0;
           } else {
             while (ii < 0) ii += H; while (ii >= H) ii -= H;
             while (jj < 0) jj += W; while (jj >= W) jj -= W;
             off = ii * W + jj;
           }
         }
-        const bool ok = off >= 0;
-        if (!ok) off = 0;
-        if (ring) {
-          const float* src = ok ? xb + 3 * HW + off : g_zero;
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                           (__attribute__((address_space(3))) void*)(al + 64 * (ii_ - NI)),
-                                           4, 0, 0);
-        } else {
-          float* dst = xs + 64 * ii_;
+        float* dst = xs + 64 * ii_;
 #pragma unroll 4
-          for (int c = 0; c < CP; ++c) {
-            const float* src = (ok && c < C) ? xb + c * HW + off : g_zero;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)(dst + c * PSTR),
-                                             4, 0, 0);
+        for (int c = 0; c < CP; ++c) {
+          const float* src = xb + (size_t)min(c, C - 1) * HW + off;
+          if ((zp && !ok) || c >= C) src = g_zero;
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)(dst + c * PSTR),
+                                           4, 0, 0);
+        }
+      }
+      // alpha plane with one more ring: element e of ((RH+2) x ALW) -> (i0-RY-1+vr, j0-RX-1+vc)
+#pragma unroll 1
+      for (int ii_ = wave; ii_ < NIA; ii_ += NW) {
+        const int e = 64 * ii_ + lane;
+        int off = 0;
+        bool ok = true;
+        if (e < (RH + 2) * ALW) {
+          const int vr = e / ALW, vc = e - (e / ALW) * ALW;
+          int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
+          if (zp) {
+            ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
+            off = ok ? ii * W + jj : 0;
+          } else {
+            while (ii < 0) ii += H; while (ii >= H) ii -= H;
+            while (jj < 0) jj += W; while (jj >= W) jj -= W;
+            off = ii * W + jj;
           }
         }
+        const float* src = xb + 3 * HW + off;
+        if (zp && !ok) src = g_zero;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(al + 64 * ii_),
+                                         4, 0, 0);
       }
     }
     // ---- per-tile side tables while the DMA is in flight: offset weights, fire plane ----
@@ -428,13 +445,16 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
       if (graph_on && !(GNCA_ABLATE & kAblGather)) {
         if constexpr (KU_ > 0) {
           // compile-time width, uniform weight 1/k applied once after the sum (exact for k=8)
+          const float* spq = sp + pidx;
+          const float* xq = xg + pidx;
 #pragma unroll
           for (int o = 0; o < KU_; ++o) {
-            const int qb = pidx - a.odl[o];
-            const float s_ = sp[qb];
+            const int d = a.odl[o];
+            const float s_ = spq[-d];
             S += s_;
+            const float* xo = xq - d;
 #pragma unroll
-            for (int t = 0; t < CPQ; ++t) gv[t] = fmaf(s_, xg[qb + 4 * t * PSTR], gv[t]);
+            for (int t = 0; t < CPQ; ++t) gv[t] = fmaf(s_, xo[4 * t * PSTR], gv[t]);
           }
           const float wu = a.uniform_w;
 #pragma unroll
