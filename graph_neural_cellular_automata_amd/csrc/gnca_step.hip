@@ -301,7 +301,15 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   const int ncell = TH * TW, ngroups = (ncell + 15) >> 4;
   const size_t HW = (size_t)H * W;
 
-  for (int tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+  // XCD-aware tile order (speed only, never correctness): workgroups b and b+8 share an XCD
+  // under round-robin dispatch, so XCD group x = b % 8 sweeps its own contiguous range of tiles
+  // with its workgroups side by side: neighbouring tiles' halo re-reads hit that XCD's L2.
+  const int nxcd = gridDim.x >= 8 ? 8 : 1;
+  const int xg_ = blockIdx.x % nxcd, xr_ = blockIdx.x / nxcd;
+  const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
+  const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
+  const int t_begin = xg_ * tq + min(xg_, trm), t_end = t_begin + tq + (xg_ < trm ? 1 : 0);
+  for (int tile = t_begin + xr_; tile < t_end; tile += per_x) {
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
