@@ -10,8 +10,23 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+def _names(pattern):
+    return sorted(os.path.splitext(os.path.basename(p))[0] for p in glob.glob(f"{GOLDEN}/{pattern}"))
+
+
 def case_names():
-    return sorted(os.path.splitext(os.path.basename(p))[0] for p in glob.glob(f"{GOLDEN}/*.npz"))
+    """Forward fixtures (make_golden.py)."""
+    return [n for n in _names("*.npz") if not n.startswith(("grad_", "bptt_"))]
+
+
+def grad_case_names():
+    """One-step gradient fixtures (make_golden_grad.py)."""
+    return _names("grad_*.npz")
+
+
+def bptt_case_names():
+    """BPTT rollout gradient fixtures (make_golden_grad.py)."""
+    return _names("bptt_*.npz")
 
 
 class Case:
@@ -37,6 +52,11 @@ class Case:
                     use_groupnorm=m["use_groupnorm"], graph=m["graph"],
                     message_gain=m["message_gain"], hidden_only=m["hidden_only"],
                     zero_padded_shift=m["zero_padded_shift"], alive_to_alive=m["alive_to_alive"])
+
+    def grads(self, f64=True):
+        """The reference's parameter gradients, keyed like the state_dict."""
+        pre = "g64:" if f64 else "g:"
+        return {k[len(pre):]: v for k, v in self.arrays.items() if k.startswith(pre)}
 
     def chosen(self, t=0):
         return [tuple(int(v) for v in o) for o in self.offsets[t]]
