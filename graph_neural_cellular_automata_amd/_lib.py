@@ -14,7 +14,7 @@ import torch  # noqa: F401  — load torch's HIP runtime first; libgnca.so binds
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgnca.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_OFFSETS = 128
 
 GRAPH = 1 << 0
@@ -51,9 +51,15 @@ class Weights(ctypes.Structure):
         "wq", "bq", "wk", "bk", "wm", "bm", "scaling")]
 
 
+class Grads(ctypes.Structure):
+    """Mirror of gnca_grads (include/gnca.h): device output pointers in reference layouts."""
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "w1", "b1", "w2", "gn_weight", "gn_bias", "wq", "bq", "wk", "bk", "wm", "bm", "scaling")]
+
+
 EXPORTS = ("gnca_abi_version", "gnca_status_string", "gnca_last_hip_error",
            "gnca_workspace_bytes", "gnca_step_f32", "gnca_step_phases_f32", "gnca_message_f32",
-           "gnca_perceive_f32", "gnca_rollout_f32")
+           "gnca_perceive_f32", "gnca_rollout_f32", "gnca_bwd_workspace_bytes", "gnca_step_bwd_f32")
 
 PHASE_K0, PHASE_K1, PHASE_K2 = 1, 2, 4
 PHASE_ALL = 7
@@ -96,6 +102,11 @@ def load(path: str = LIB_PATH):
     lib.gnca_rollout_f32.restype = ctypes.c_int
     lib.gnca_rollout_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights),
                                      ctypes.c_int32, vp, vp, vp, vp, vp, sz, vp]
+    lib.gnca_bwd_workspace_bytes.restype = sz
+    lib.gnca_bwd_workspace_bytes.argtypes = [ctypes.POINTER(StepDesc)]
+    lib.gnca_step_bwd_f32.restype = ctypes.c_int
+    lib.gnca_step_bwd_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights), vp, vp, vp,
+                                      vp, ctypes.POINTER(Grads), vp, sz, vp]
     v = lib.gnca_abi_version()
     if v != ABI_VERSION:
         raise GncaError(f"libgnca.so ABI version {v} != expected {ABI_VERSION}; rebuild it")

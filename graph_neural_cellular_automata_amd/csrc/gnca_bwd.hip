@@ -1,0 +1,1383 @@
+// gnca_bwd.hip — MI355X (gfx950 / CDNA4) backward of the NCA step (BPTT), SURVEY.md §8f rank 1.
+//
+// The vector-Jacobian product of one step (reference forward: src/modules/ncagraph.py:106-168,
+// src/modules/nca.py:64-105, src/modules/graph_augmentation.py:104-169; the reference gets its
+// gradients from torch autograd in the trainers' loss.backward(),
+// src/training/train_graph_augmented_nca.py:369).  Restated in numpy by
+// oracle/nca_oracle_vjp.py (test infrastructure), which is pinned to the reference's autograd.
+//
+// Nothing is saved by the forward: the backward recomputes it.
+//
+//   F   forward K0/K1 (gnca_step.hip) into the workspace: dx (pre-GroupNorm update, masked),
+//       per-tile GroupNorm partials, zero-pad offset weights.
+//   BA  gnca_b_gnprep     per (sample, row band): post-update gate (3x3 halo), tanh', GroupNorm
+//                         backward prep:  gx = gy*gate (the residual),  U = gamma*g_xn,
+//                         fp64 partials of sum U, sum U*xhat (per sample) and of the norm
+//                         weight/bias gradients (per channel).
+//   BS  gnca_b_coef       per sample: mean, rstd, mean(U), mean(U*xhat).
+//   BB  gnca_b_mlp<CP,HB> the MFMA kernel, persistent, one hidden slice of HB units per launch:
+//                         recompute perception / gather / GEMM1 / message, then
+//                           d_pre = keep * rstd*(U - mean U - xhat*mean(U xhat))   (GN backward)
+//                           dh = relu'(h) * W2^T d_pre        (MFMA)
+//                           dY = W1^T dh     -> HBM           (MFMA; the perception adjoint's input)
+//                           dm = d_pre*gain*tanh'(m); dG = W_M^T dm -> HBM  (MFMA)
+//                         and the weight gradients dW1 = dh y^T, dW2 = d_pre h^T, dW_M = dm G^T
+//                         on MFMA with the cell dimension as K (per-wave LDS transposes; per-wave
+//                         register accumulators for the whole launch), db1, db_M.
+//   BC  gnca_b_adjoint    gx += Sobel^T dY + A_send * sum_o w_o dG(q+o)  (adjoint of the
+//                         zero-padded 3x3 correlation and of the rolled / row-shifted gather).
+//   zero-pad mode only (offset weights depend on x, Q, K, scaling):
+//   BC2 gnca_b_dots       per (sample, offset): dL/dw_o = sum_q A(q) (<dG(q+o), x(q)> + <dm(q+o), b_M>)
+//   BD  gnca_b_attn       softmax / pooled-logit backward per sample (fp64): Q, K, scaling grads,
+//                         and the per-row correction of gx through the pooled means.
+//   BE  gnca_b_rowcorr    gx += corr[b, row, c].
+//   R   gnca_b_reduce     fixed-order sums of the per-wave / per-band / per-sample partials into
+//                         the caller's gradient buffers (deterministic: no float atomics).
+
+#include <algorithm>
+#include <cstdlib>
+#include <mutex>
+#include <unordered_map>
+
+#include "gnca_device.h"
+
+namespace gnca {
+namespace {
+
+constexpr int NW = kThreads / 64;
+constexpr uint32_t kMsg = 1u << 16;      // message path active (k > 0 and message_gain != 0)
+constexpr uint32_t kFirst = 1u << 17;    // first hidden slice: also the message backward
+constexpr uint32_t kGN = 1u << 18;       // GroupNorm on
+
+__host__ __device__ inline int s16(int v) {  // >= v, multiple of 16, == 16 mod 32 (bank spread)
+  const int s = (v + 15) & ~15;
+  return (s & 31) == 16 ? s : s + 16;
+}
+
+__device__ __forceinline__ double2 block_sum2(double a, double b, double* red) {
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off);
+    b += __shfl_xor(b, off);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[2 * wave] = a;
+    red[2 * wave + 1] = b;
+  }
+  __syncthreads();
+  double ta = 0.0, tb = 0.0;
+  for (int w = 0; w < NW; ++w) {  // fixed order: deterministic
+    ta += red[2 * w];
+    tb += red[2 * w + 1];
+  }
+  __syncthreads();
+  return make_double2(ta, tb);
+}
+
+__device__ __forceinline__ void sample_stats(const double* stats, int b, int tps, double n, float eps,
+                                             float* mu, float* rs) {
+  double t1 = 0.0, t2 = 0.0;  // the forward K2's fixed-order sum (same values bit for bit)
+  for (int t = 0; t < tps; ++t) {
+    t1 += stats[((size_t)b * tps + t) * 2];
+    t2 += stats[((size_t)b * tps + t) * 2 + 1];
+  }
+  const double m = t1 / n;
+  double var = t2 / n - m * m;
+  if (var < 0.0) var = 0.0;
+  *mu = (float)m;
+  *rs = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// ------------------------------------------------------------------------------------------
+// BA: gate / tanh / GroupNorm backward prep (ncagraph.py:153-166)
+// ------------------------------------------------------------------------------------------
+struct BAArgs {
+  const float* x;
+  const float* dx;
+  const float* gy;
+  const float* gamma;
+  const float* beta;
+  const double* stats;
+  float* gx;
+  float* U;
+  double* part;   // [B * nbands][2 + 2C]: sum U, sum U*xhat, then (sum g_xn*xhat, sum g_xn) per c
+  int B, C, H, W, tps, band, nbands;
+  float gain, thr, eps;
+  int use_gn;
+};
+
+__global__ __launch_bounds__(kThreads) void gnca_b_gnprep(const BAArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ double red[2 * NW];
+  __shared__ float sh[2];
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x / a.nbands, band = blockIdx.x - b * a.nbands;
+  const int C = a.C, H = a.H, W = a.W;
+  const int r0 = band * a.band, r1 = min(H, r0 + a.band);
+  const int h0 = max(0, r0 - 1), h1 = min(H, r1 + 1);
+  const size_t HW = (size_t)H * W;
+  const bool gn = a.use_gn != 0;
+  if (tid == 0) {
+    float mu = 0.f, rs = 1.f;
+    if (gn) sample_stats(a.stats, b, a.tps, (double)C * (double)HW, a.eps, &mu, &rs);
+    sh[0] = mu;
+    sh[1] = rs;
+  }
+  __syncthreads();
+  const float mu = sh[0], rs = sh[1];
+  const float* xb = a.x + (size_t)b * C * HW;
+  const float* db = a.dx + (size_t)b * C * HW;
+  const float* gb = a.gy + (size_t)b * C * HW;
+  float* gxb = a.gx + (size_t)b * C * HW;
+  float* ub = a.U + (size_t)b * C * HW;
+  float* at = smem;                                  // updated alpha, band rows + halo
+  float* post = smem + (size_t)(a.band + 2) * W;     // post-update alive mask of the band
+  {
+    const float g3 = gn ? a.gamma[3] : 1.f, b3 = gn ? a.beta[3] : 0.f;
+    const int na = (h1 - h0) * W;
+    for (int e = tid; e < na; e += kThreads) {
+      const size_t p = 3 * HW + (size_t)h0 * W + e;
+      float d = db[p];
+      if (gn) d = (d - mu) * rs * g3 + b3;   // the forward K2's expression for alpha
+      at[e] = xb[p] + tanhf(d) * a.gain;
+    }
+  }
+  __syncthreads();
+  const int nb = (r1 - r0) * W;
+  for (int e = tid; e < nb; e += kThreads) {
+    const int i = r0 + e / W, j = e - (e / W) * W;
+    float mx = -INFINITY;
+    for (int ii = max(0, i - 1); ii <= min(H - 1, i + 1); ++ii) {
+      const float* row = at + (size_t)(ii - h0) * W;
+      mx = fmaxf(mx, row[j]);
+      if (j > 0) mx = fmaxf(mx, row[j - 1]);
+      if (j < W - 1) mx = fmaxf(mx, row[j + 1]);
+    }
+    post[e] = mx > a.thr ? 1.f : 0.f;
+  }
+  __syncthreads();
+  const size_t base = (size_t)r0 * W;
+  double su = 0.0, sux = 0.0;
+  double* outp = a.part + (size_t)blockIdx.x * (2 + 2 * C);
+  for (int c = 0; c < C; ++c) {
+    const float gc = gn ? a.gamma[c] : 1.f, bc = gn ? a.beta[c] : 0.f;
+    const float gcr = gc * rs;
+    double sg = 0.0, sgx = 0.0;
+    for (int e = tid; e < nb; e += kThreads) {
+      const size_t p = (size_t)c * HW + base + e;
+      const float d = db[p];
+      const float xhat = (d - mu) * rs;
+      const float xn = gn ? (c == 3 ? (d - mu) * rs * gc + bc : (d - mu) * gcr + bc) : d;
+      const float t = tanhf(xn);
+      float g = gb[p];
+      if (c == 3) g *= post[e];                       // x * gate, gate on alpha only (:158-166)
+      gxb[p] = g;                                     // the residual x + ... (:155)
+      const float gxn = g * a.gain * (1.f - t * t);   // tanh(.)*update_gain (:154)
+      const float u = gn ? gxn * gc : gxn;
+      ub[p] = u;
+      sg += (double)gxn;
+      sgx += (double)gxn * (double)xhat;
+      su += (double)u;
+      sux += (double)u * (double)xhat;
+    }
+    const double2 r = block_sum2(sgx, sg, red);
+    if (tid == 0) {
+      outp[2 + 2 * c] = r.x;
+      outp[3 + 2 * c] = r.y;
+    }
+  }
+  const double2 r = block_sum2(su, sux, red);
+  if (tid == 0) {
+    outp[0] = r.x;
+    outp[1] = r.y;
+  }
+}
+
+// BS: per-sample GroupNorm-backward coefficients (mu, rstd, mean U, mean U*xhat)
+__global__ __launch_bounds__(kThreads) void gnca_b_coef(const double* stats, const double* part,
+                                                        float* coef, int B, int C, int HW, int tps,
+                                                        int nbands, float eps, int use_gn) {
+  const int b = blockIdx.x * kThreads + threadIdx.x;
+  if (b >= B) return;
+  float mu = 0.f, rs = 1.f, mu_u = 0.f, mu_ux = 0.f;
+  if (use_gn) {
+    const double n = (double)C * (double)HW;
+    sample_stats(stats, b, tps, n, eps, &mu, &rs);
+    double su = 0.0, sux = 0.0;
+    for (int t = 0; t < nbands; ++t) {
+      su += part[((size_t)b * nbands + t) * (2 + 2 * C)];
+      sux += part[((size_t)b * nbands + t) * (2 + 2 * C) + 1];
+    }
+    mu_u = (float)(su / n);
+    mu_ux = (float)(sux / n);
+  }
+  coef[4 * b + 0] = mu;
+  coef[4 * b + 1] = rs;
+  coef[4 * b + 2] = mu_u;
+  coef[4 * b + 3] = mu_ux;
+}
+
+// ------------------------------------------------------------------------------------------
+// BB: the MFMA kernel
+// ------------------------------------------------------------------------------------------
+struct BBLayout {
+  int xs, PSTR, al, ALW, sp, kp, w1s, SW1, w2s, SW2, wms, SWM, b1s, bms, percs, wts, scr;
+  int ST1, ST2, ST3, SCRW, RH, RW, total;
+};
+
+__host__ __device__ inline BBLayout bb_layout(int CP, int HB, int TH, int TW, int RY, int RX, int kmax) {
+  BBLayout L;
+  L.RH = TH + 2 * RY;
+  L.RW = TW + 2 * RX;
+  L.PSTR = r4(L.RH * L.RW);
+  L.ALW = L.RW + 2;
+  const int CPM = 16 * ((CP + 15) / 16);   // channel rows padded to whole 16-row MFMA tiles
+  L.SW1 = odd4(3 * CP);
+  L.SW2 = odd4(HB);
+  L.SWM = odd4(CPM);
+  L.ST1 = s16(HB);
+  L.ST2 = s16(3 * CP);
+  L.ST3 = s16(CP);
+  L.SCRW = 16 * (L.ST1 + L.ST2 + 2 * L.ST3);
+  int o = 0;
+  L.xs = o; o += CP * L.PSTR;
+  L.al = o; o += r4((L.RH + 2) * L.ALW);
+  L.sp = o; o += r4(L.RH * L.RW);
+  L.kp = o; o += r4(TH * TW);
+  L.w1s = o; o += HB * L.SW1;
+  L.w2s = o; o += CPM * L.SW2;    // zero rows past C: the MFMA tiles read all 16*MO rows
+  L.wms = o; o += CPM * L.SWM;
+  L.b1s = o; o += r4(HB);
+  L.bms = o; o += CPM;
+  L.percs = o; o += CP * 36;
+  L.wts = o; o += r4(kmax > 0 ? kmax : 4);
+  L.scr = o; o += NW * L.SCRW;
+  L.total = o;
+  return L;
+}
+
+struct BBArgs {
+  const float* x;
+  const float* U;
+  const float* dx;
+  const float* coef;
+  const void* fire;
+  const float* perc;
+  const float* w1;
+  const float* b1;
+  const float* w2;
+  const float* wm;
+  const float* bm;
+  const float* offw;   // [B*k] zero-pad weights or null (uniform 1/k)
+  float* dY;           // [B, 3C, H, W]
+  float* dG;           // [B, C, H, W]
+  float* dmb;          // [B, H, W] <dm, b_M> (zero-pad only) or null
+  float* part;         // [gridDim.x * NW][npart]
+  uint64_t seed;
+  int64_t rng_step;
+  int64_t sample_base;
+  int B, C, H, W, hidden, h0, k, RY, RX, TH, TW, tiles_x, tps, total_tiles, fire_mode;
+  int npart, o_w1, o_b1, o_w2, o_wm, o_bm;
+  float fire_rate, alpha_thr, graph_alpha_thr, message_gain, uniform_w;
+  uint32_t flags;
+  int odl[GNCA_MAX_OFFSETS];
+};
+
+template <int CP, int HB>
+__global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int CPQ = CP / 4, KS = 3 * CPQ, MT = HB / 16, MO = (CP + 15) / 16, FT = (3 * CP + 15) / 16;
+  const int TH = a.TH, TW = a.TW, RY = a.RY, RX = a.RX;
+  const BBLayout L = bb_layout(CP, HB, TH, TW, RY, RX, a.k);
+  const int RH = L.RH, RW = L.RW, PSTR = L.PSTR, ALW = L.ALW;
+  const int SW1 = L.SW1, SW2 = L.SW2, SWM = L.SWM, ST1 = L.ST1, ST2 = L.ST2, ST3 = L.ST3;
+  float* xs = smem + L.xs;
+  float* al = smem + L.al;
+  float* sp = smem + L.sp;
+  float* fp = smem + L.kp;
+  float* w1s = smem + L.w1s;
+  float* w2s = smem + L.w2s;
+  float* wms = smem + L.wms;
+  float* b1s = smem + L.b1s;
+  float* bms = smem + L.bms;
+  float* percs = smem + L.percs;
+  float* wts = smem + L.wts;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int C = a.C, H = a.H, W = a.W, Hd = a.hidden, h0 = a.h0, k = a.k;
+  const bool zp = (a.flags & GNCA_ZERO_PAD_SHIFT) != 0;
+  const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
+  const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
+  const bool msg = (a.flags & kMsg) != 0;
+  const bool first = (a.flags & kFirst) != 0;
+  const bool msg_bwd = msg && first;
+  const bool gn = (a.flags & kGN) != 0;
+  const bool uniform_w = a.offw == nullptr;
+  const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
+  float* T1 = smem + L.scr + wave * L.SCRW;   // per-wave transpose scratch [16 cells][...]
+  float* T2 = T1 + 16 * ST1;
+  float* T3 = T2 + 16 * ST2;
+  float* T4 = T3 + 16 * ST3;
+
+  // ---- weights of this hidden slice -> LDS (row-major; strides chosen bank-conflict-free for
+  //      both the forward (W1) and the transposed (W1^T, W2^T, W_M^T) fragment reads) ----
+  for (int idx = tid; idx < HB * SW1; idx += kThreads) {
+    const int r = idx / SW1, slot = idx - r * SW1, hid = h0 + r;
+    const int f = slot / CP, c = slot - f * CP;
+    w1s[idx] = (hid < Hd && slot < 3 * CP && c < C) ? a.w1[(size_t)hid * 3 * C + f * C + c] : 0.f;
+  }
+  for (int idx = tid; idx < 16 * MO * SW2; idx += kThreads) {
+    const int c = idx / SW2, col = idx - c * SW2, hid = h0 + col;
+    w2s[idx] = (c < C && col < HB && hid < Hd) ? a.w2[(size_t)c * Hd + hid] : 0.f;
+  }
+  for (int idx = tid; idx < 16 * MO * SWM; idx += kThreads) {
+    const int co = idx / SWM, ci = idx - co * SWM;
+    wms[idx] = (msg && co < C && ci < C) ? a.wm[co * C + ci] : 0.f;
+  }
+  for (int idx = tid; idx < HB; idx += kThreads) b1s[idx] = h0 + idx < Hd ? a.b1[h0 + idx] : 0.f;
+  for (int idx = tid; idx < 16 * MO; idx += kThreads) bms[idx] = (msg && idx < C) ? a.bm[idx] : 0.f;
+  for (int idx = tid; idx < CP * 36; idx += kThreads) {
+    const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
+    percs[idx] = (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
+  }
+  __syncthreads();
+  bool sobel;
+  {
+    int ok = 1;
+    for (int idx = tid; idx < C * 27; idx += kThreads) {
+      const int c = idx / 27, e = idx % 27, f = e / 9, tap = e % 9;
+      const int tr = tap / 3, tc = tap % 3;
+      float ref;
+      if (f == 0) ref = (tap == 4) ? 1.f : 0.f;
+      else if (f == 1) ref = (float)((tc == 0 ? 1 : (tc == 2 ? -1 : 0)) * (tr == 1 ? 2 : 1));
+      else ref = (float)((tr == 0 ? 1 : (tr == 2 ? -1 : 0)) * (tc == 1 ? 2 : 1));
+      if (percs[c * 36 + f * 12 + tap] != ref) ok = 0;
+    }
+    sobel = __syncthreads_and(ok) != 0;
+  }
+  float gainr[MO];
+#pragma unroll
+  for (int mo = 0; mo < MO; ++mo)
+    gainr[mo] = (msg && !(hidden_only && mo == 0 && g == 0)) ? a.message_gain : 0.f;
+
+  // per-wave accumulators of the whole launch (AGPR-resident)
+  f4 aw1[MT][FT], aw2[MO][MT], awm[MO][MO], abm[MO];
+  float ab1[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    ab1[m] = 0.f;
+#pragma unroll
+    for (int f = 0; f < FT; ++f) aw1[m][f] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int mo = 0; mo < MO; ++mo) {
+    abm[mo] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < MT; ++m) aw2[mo][m] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mi = 0; mi < MO; ++mi) awm[mo][mi] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int ncell = TH * TW, ngroups = (ncell + 15) >> 4;
+  const size_t HW = (size_t)H * W;
+  for (int tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+    const int b = tile / a.tps, tin = tile - b * a.tps;
+    const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+    const int i0 = ty * TH, j0 = tx * TW;
+    const float* xb = a.x + (size_t)b * C * HW;
+    __syncthreads();
+    // ---- staging: channel planes over the (RH x RW) region, alpha with one more ring ----
+    for (int e = tid; e < CP * RH * RW; e += kThreads) {
+      const int c = e / (RH * RW), pos = e - c * (RH * RW);
+      const int vr = pos / RW, vc = pos - vr * RW;
+      int ii = i0 - RY + vr, jj = j0 - RX + vc;
+      bool ok = true;
+      if (zp) ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
+      else { ii = wrapi(ii, H); jj = wrapi(jj, W); }
+      xs[c * PSTR + pos] = (ok && c < C) ? xb[(size_t)c * HW + (size_t)ii * W + jj] : 0.f;
+    }
+    for (int e = tid; e < (RH + 2) * ALW; e += kThreads) {
+      const int vr = e / ALW, vc = e - vr * ALW;
+      int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
+      bool ok = true;
+      if (zp) ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
+      else { ii = wrapi(ii, H); jj = wrapi(jj, W); }
+      al[e] = ok ? xb[3 * HW + (size_t)ii * W + jj] : 0.f;
+    }
+    if (msg && !uniform_w)
+      for (int o = tid; o < k; o += kThreads) wts[o] = a.offw[(size_t)b * k + o];
+    for (int n = tid; n < ncell; n += kThreads) {
+      const int ti = n / TW, tj = n - (n / TW) * TW;
+      const int i = min(i0 + ti, H - 1), j = min(j0 + tj, W - 1);
+      fp[n] = fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step, a.sample_base, b, HW,
+                      (size_t)i * W + j) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    // ---- sender plane over the region, keep = pre-alive AND fire on the tile (as K1) ----
+    for (int pos = tid; pos < RH * RW; pos += kThreads) {
+      const int vr = pos / RW, vc = pos - vr * RW;
+      int iq = i0 - RY + vr, jq = j0 - RX + vc;
+      bool in_img = true;
+      if (zp) in_img = iq >= 0 && iq < H && jq >= 0 && jq < W;
+      else { iq = wrapi(iq, H); jq = wrapi(jq, W); }
+      const float* q = al + (vr + 1) * ALW + (vc + 1);
+      const float NEG = -INFINITY;
+      const bool up = iq > 0, dn = iq < H - 1, lf = jq > 0, rt = jq < W - 1;
+      const float mu_ = fmaxf(fmaxf(lf ? q[-ALW - 1] : NEG, q[-ALW]), rt ? q[-ALW + 1] : NEG);
+      const float mm_ = fmaxf(fmaxf(lf ? q[-1] : NEG, q[0]), rt ? q[1] : NEG);
+      const float md_ = fmaxf(fmaxf(lf ? q[ALW - 1] : NEG, q[ALW]), rt ? q[ALW + 1] : NEG);
+      const float mx = fmaxf(fmaxf(up ? mu_ : NEG, mm_), dn ? md_ : NEG);
+      sp[pos] = a2a ? ((in_img && mx > gthr) ? 1.f : 0.f) : (in_img ? 1.f : 0.f);
+      const int ti = vr - RY, tj = vc - RX;
+      if (ti >= 0 && ti < TH && tj >= 0 && tj < TW) {
+        const int n = ti * TW + tj;
+        fp[n] = (in_img && mx > thr) ? fp[n] : 0.f;
+      }
+    }
+    __syncthreads();
+    const float mu = a.coef[4 * b], rs = a.coef[4 * b + 1];
+    const float mu_u = a.coef[4 * b + 2], mu_ux = a.coef[4 * b + 3];
+
+#pragma unroll 1
+    for (int q = wave; q < ngroups; q += NW) {
+      const int n = 16 * q + c16;
+      int ti = n / TW, tj = n - (n / TW) * TW;
+      const bool valid = n < ncell && i0 + ti < H && j0 + tj < W;
+      if (!valid) { ti = 0; tj = 0; }
+      const int pidx = (RY + ti) * RW + (RX + tj);
+      const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
+      const float* xg = xs + g * PSTR;
+
+      // -- gather (recompute) --
+      float gv[CPQ];
+#pragma unroll
+      for (int t = 0; t < CPQ; ++t) gv[t] = 0.f;
+      float S = 0.f;
+      if (msg) {
+        for (int o = 0; o < k; ++o) {
+          const int qb = pidx - a.odl[o];
+          const float wsp = (uniform_w ? a.uniform_w : wts[o]) * sp[qb];
+          S += wsp;
+#pragma unroll
+          for (int t = 0; t < CPQ; ++t) gv[t] = fmaf(wsp, xg[qb + 4 * t * PSTR], gv[t]);
+        }
+      }
+      // -- perception (recompute) --
+      float y[KS];
+      {
+        const int ic = i0 + ti, jc = j0 + tj;
+        const bool up = ic > 0, dn = ic < H - 1, lf = jc > 0, rt = jc < W - 1;
+#pragma unroll
+        for (int t = 0; t < CPQ; ++t) {
+          const float* xc = xg + 4 * t * PSTR + pidx;
+          float n0 = xc[-RW - 1], n1 = xc[-RW], n2 = xc[-RW + 1];
+          float n3 = xc[-1], n4 = xc[0], n5 = xc[1];
+          float n6 = xc[RW - 1], n7 = xc[RW], n8 = xc[RW + 1];
+          n0 = (up && lf) ? n0 : 0.f; n1 = up ? n1 : 0.f; n2 = (up && rt) ? n2 : 0.f;
+          n3 = lf ? n3 : 0.f;                               n5 = rt ? n5 : 0.f;
+          n6 = (dn && lf) ? n6 : 0.f; n7 = dn ? n7 : 0.f; n8 = (dn && rt) ? n8 : 0.f;
+          if (sobel) {
+            y[t] = n4;
+            y[CPQ + t] = (fmaf(2.f, n3, n0) + n6) - (fmaf(2.f, n5, n2) + n8);
+            y[2 * CPQ + t] = (fmaf(2.f, n1, n0) + n2) - (fmaf(2.f, n7, n6) + n8);
+          } else {
+            const int c = 4 * t + g;
+            const f4* pw = reinterpret_cast<const f4*>(percs + c * 36);
+#pragma unroll
+            for (int f = 0; f < 3; ++f) {
+              const f4 w0 = pw[3 * f], w1 = pw[3 * f + 1], w2 = pw[3 * f + 2];
+              float acc = w0[0] * n0;
+              acc = fmaf(w0[1], n1, acc); acc = fmaf(w0[2], n2, acc); acc = fmaf(w0[3], n3, acc);
+              acc = fmaf(w1[0], n4, acc); acc = fmaf(w1[1], n5, acc); acc = fmaf(w1[2], n6, acc);
+              acc = fmaf(w1[3], n7, acc); acc = fmaf(w2[0], n8, acc);
+              y[f * CPQ + t] = acc;
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // -- GEMM1 (recompute): hpre[hid = 16m+4g+r][cell] --
+      f4 hp[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) hp[m] = *reinterpret_cast<const f4*>(b1s + 16 * m + 4 * g);
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          hp[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1s[(16 * m + c16) * SW1 + 4 * s + g], y[s], hp[m], 0, 0, 0);
+      // -- message (recompute): m[c = 16mo+4g+r][cell] = W_M G + b_M S --
+      f4 mm[MO];
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo) mm[mo] = f4{0.f, 0.f, 0.f, 0.f};
+      if (msg_bwd) {
+#pragma unroll
+        for (int s = 0; s < CPQ; ++s)
+#pragma unroll
+          for (int mo = 0; mo < MO; ++mo)
+            mm[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wms[(16 * mo + c16) * SWM + 4 * s + g], gv[s], mm[mo], 0, 0, 0);
+#pragma unroll
+        for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mm[mo][r] = fmaf(bms[16 * mo + 4 * g + r], S, mm[mo][r]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // -- d_pre = keep * GroupNorm-backward(U) (ncagraph.py:144-153) --
+      const float keep = fp[valid ? n : 0];
+      f4 dp[MO];
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 16 * mo + 4 * g + r;
+          float v = 0.f;
+          if (valid && c < C && keep != 0.f) {
+            const size_t p = ((size_t)b * C + c) * HW + cell;
+            const float u = a.U[p];
+            v = gn ? rs * (u - mu_u - (a.dx[p] - mu) * rs * mu_ux) : u;
+          }
+          dp[mo][r] = v;
+        }
+      // -- dh = relu'(hpre) * W2^T d_pre --
+      f4 dh[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) dh[m] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            dh[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2s[(16 * mo + 4 * g + s) * SW2 + 16 * m + c16],
+                                                         dp[mo][s], dh[m], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dh[m][r] = hp[m][r] > 0.f ? dh[m][r] : 0.f;
+          hp[m][r] = hp[m][r] > 0.f ? hp[m][r] : (hp[m][r] != hp[m][r] ? hp[m][r] : 0.f);  // relu
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      // -- dY = W1^T dh -> HBM (slot = f*CP + c -> plane f*C + c) --
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        f4 ay = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ay = __builtin_amdgcn_mfma_f32_16x16x4f32(w1s[(16 * m + 4 * g + r) * SW1 + 16 * ft + c16],
+                                                      dh[m][r], ay, 0, 0, 0);
+        if (valid) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int slot = 16 * ft + 4 * g + r;
+            if (slot >= 3 * CP) continue;
+            const int f = slot / CP, c = slot - f * CP;
+            if (c >= C) continue;
+            float* p = a.dY + ((size_t)b * 3 * C + f * C + c) * HW + cell;
+            *p = first ? ay[r] : *p + ay[r];
+          }
+        }
+      }
+      // -- message backward: dm = d_pre*gain*tanh'(m), dG = W_M^T dm -> HBM --
+      f4 dm[MO];
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo) dm[mo] = f4{0.f, 0.f, 0.f, 0.f};
+      if (msg_bwd) {
+        float dmb = 0.f;
+#pragma unroll
+        for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float t = tanhf(mm[mo][r]);
+            dm[mo][r] = dp[mo][r] * gainr[mo] * (1.f - t * t);
+            abm[mo][r] = fmaf(dm[mo][r], S, abm[mo][r]);
+            dmb = fmaf(dm[mo][r], bms[16 * mo + 4 * g + r], dmb);
+          }
+#pragma unroll
+        for (int mi = 0; mi < MO; ++mi) {
+          f4 ag = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+              ag = __builtin_amdgcn_mfma_f32_16x16x4f32(wms[(16 * mo + 4 * g + s) * SWM + 16 * mi + c16],
+                                                        dm[mo][s], ag, 0, 0, 0);
+          if (valid)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int ci = 16 * mi + 4 * g + r;
+              if (ci < C) a.dG[((size_t)b * C + ci) * HW + cell] = ag[r];
+            }
+        }
+        if (a.dmb) {
+          dmb += __shfl_xor(dmb, 16);
+          dmb += __shfl_xor(dmb, 32);
+          if (valid && g == 0) a.dmb[(size_t)b * HW + cell] = dmb;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // -- weight gradients, the cell dimension as the MFMA K (per-wave LDS transposes) --
+#pragma unroll
+      for (int m = 0; m < MT; ++m) *reinterpret_cast<f4*>(T1 + c16 * ST1 + 16 * m + 4 * g) = dh[m];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) T2[c16 * ST2 + 4 * s + g] = y[s];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int row = 4 * s4 + g;
+        float bv[FT];
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) bv[ft] = T2[row * ST2 + 16 * ft + c16];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const float av = T1[row * ST1 + 16 * m + c16];
+          ab1[m] += av;
+#pragma unroll
+          for (int ft = 0; ft < FT; ++ft)
+            aw1[m][ft] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[ft], aw1[m][ft], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) *reinterpret_cast<f4*>(T1 + c16 * ST1 + 16 * m + 4 * g) = hp[m];
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo) *reinterpret_cast<f4*>(T3 + c16 * ST3 + 16 * mo + 4 * g) = dp[mo];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int row = 4 * s4 + g;
+#pragma unroll
+        for (int mo = 0; mo < MO; ++mo) {
+          const float av = T3[row * ST3 + 16 * mo + c16];
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            aw2[mo][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, T1[row * ST1 + 16 * m + c16], aw2[mo][m], 0, 0, 0);
+        }
+      }
+      if (msg_bwd) {
+#pragma unroll
+        for (int mo = 0; mo < MO; ++mo) *reinterpret_cast<f4*>(T3 + c16 * ST3 + 16 * mo + 4 * g) = dm[mo];
+#pragma unroll
+        for (int t = 0; t < CPQ; ++t) T4[c16 * ST3 + 4 * t + g] = gv[t];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int row = 4 * s4 + g;
+#pragma unroll
+          for (int mo = 0; mo < MO; ++mo) {
+            const float av = T3[row * ST3 + 16 * mo + c16];
+#pragma unroll
+            for (int mi = 0; mi < MO; ++mi)
+              awm[mo][mi] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, T4[row * ST3 + 16 * mi + c16], awm[mo][mi], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+
+  // ---- this wave's partial gradients -> its own row (reduced later in a fixed order) ----
+  float* outp = a.part + ((size_t)blockIdx.x * NW + wave) * a.npart;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hid = h0 + 16 * m + 4 * g + r, slot = 16 * ft + c16;
+        const int f = slot / CP, c = slot - f * CP;
+        if (hid < Hd && slot < 3 * CP && c < C) outp[a.o_w1 + (size_t)hid * 3 * C + f * C + c] = aw1[m][ft][r];
+      }
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    float v = ab1[m];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    const int hid = h0 + 16 * m + c16;
+    if (g == 0 && hid < Hd) outp[a.o_b1 + hid] = v;
+  }
+#pragma unroll
+  for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 16 * mo + 4 * g + r, hid = h0 + 16 * m + c16;
+        if (c < C && hid < Hd) outp[a.o_w2 + (size_t)c * Hd + hid] = aw2[mo][m][r];
+      }
+  if (first) {
+#pragma unroll
+    for (int mo = 0; mo < MO; ++mo) {
+#pragma unroll
+      for (int mi = 0; mi < MO; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = 16 * mo + 4 * g + r, ci = 16 * mi + c16;
+          if (co < C && ci < C) outp[a.o_wm + co * C + ci] = awm[mo][mi][r];
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = abm[mo][r];
+        for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        const int co = 16 * mo + 4 * g + r;
+        if (c16 == 0 && co < C) outp[a.o_bm + co] = v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// BC: adjoint of the perception (zero-padded 3x3 correlation) and of the gather
+// ------------------------------------------------------------------------------------------
+struct BCArgs {
+  const float* dY;
+  const float* dG;
+  const float* x;
+  const float* perc;
+  const float* offw;
+  float* gx;
+  int B, C, H, W, k, TH, TW, tiles_x, tps, RY, RX;
+  float graph_alpha_thr, uniform_w;
+  uint32_t flags;
+  int8_t offs[2 * GNCA_MAX_OFFSETS];
+};
+
+__global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x / a.tps, tin = blockIdx.x - b * a.tps;
+  const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+  const int TH = a.TH, TW = a.TW, RY = a.RY, RX = a.RX, H = a.H, W = a.W, C = a.C, k = a.k;
+  const int i0 = ty * TH, j0 = tx * TW;
+  const size_t HW = (size_t)H * W;
+  const bool zp = (a.flags & GNCA_ZERO_PAD_SHIFT) != 0;
+  const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
+  const bool msg = (a.flags & kMsg) != 0;
+  const int PW = TW + 2, PA = (TH + 2) * PW;          // ring-1 planes
+  const int GW = TW + 2 * RX, GA = (TH + 2 * RY) * GW;  // gather-halo plane
+  float* dy3 = smem;                  // 3 x PA
+  float* dgp = dy3 + 3 * PA;          // GA
+  float* as_ = dgp + GA;              // TH*TW sender mask of the tile cells
+  float* wts = as_ + TH * TW;         // k
+  float* alr = wts + (k > 0 ? k : 1); // PA alpha ring (-inf outside)
+  const float* xb = a.x + (size_t)b * C * HW;
+  if (msg) {
+    for (int e = tid; e < PA; e += kThreads) {
+      const int ii = i0 - 1 + e / PW, jj = j0 - 1 + e % PW;
+      alr[e] = (ii >= 0 && ii < H && jj >= 0 && jj < W) ? xb[3 * HW + (size_t)ii * W + jj] : -INFINITY;
+    }
+    for (int o = tid; o < k; o += kThreads) wts[o] = a.offw ? a.offw[(size_t)b * k + o] : a.uniform_w;
+    __syncthreads();
+    for (int n = tid; n < TH * TW; n += kThreads) {
+      const int ti = n / TW, tj = n % TW;
+      float mx = -INFINITY;
+      for (int u = 0; u < 3; ++u)
+        for (int v = 0; v < 3; ++v) mx = fmaxf(mx, alr[(ti + u) * PW + tj + v]);
+      as_[n] = a2a ? (mx > a.graph_alpha_thr ? 1.f : 0.f) : 1.f;
+    }
+  }
+  for (int c = 0; c < C; ++c) {
+    __syncthreads();
+    for (int e = tid; e < 3 * PA; e += kThreads) {
+      const int f = e / PA, r = e - f * PA;
+      const int ii = i0 - 1 + r / PW, jj = j0 - 1 + r % PW;
+      dy3[e] = (ii >= 0 && ii < H && jj >= 0 && jj < W)
+                   ? a.dY[((size_t)b * 3 * C + f * C + c) * HW + (size_t)ii * W + jj] : 0.f;
+    }
+    if (msg)
+      for (int e = tid; e < GA; e += kThreads) {
+        int ii = i0 - RY + e / GW, jj = j0 - RX + e % GW;
+        bool ok = true;
+        if (zp) ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
+        else { ii = wrapi(ii, H); jj = wrapi(jj, W); }
+        dgp[e] = ok ? a.dG[((size_t)b * C + c) * HW + (size_t)ii * W + jj] : 0.f;
+      }
+    __syncthreads();
+    const float* pw = a.perc + (size_t)3 * c * 9;
+    for (int n = tid; n < TH * TW; n += kThreads) {
+      const int ti = n / TW, tj = n % TW;
+      const int i = i0 + ti, j = j0 + tj;
+      if (i >= H || j >= W) continue;
+      // y(p) += w[u][v] x(p + (u-1, v-1))  =>  gx(q) += w[u][v] dY(q - (u-1, v-1))
+      float acc = 0.f;
+      for (int f = 0; f < 3; ++f)
+        for (int u = 0; u < 3; ++u)
+          for (int v = 0; v < 3; ++v)
+            acc = fmaf(pw[f * 9 + u * 3 + v], dy3[f * PA + (ti + 2 - u) * PW + (tj + 2 - v)], acc);
+      if (msg) {
+        // msg(p) = sum_o w_o A(p-o) M(p-o)  =>  gM(q) = A(q) sum_o w_o dm(q+o)  (roll / row shift)
+        float sg = 0.f;
+        for (int o = 0; o < k; ++o) {
+          const int dy = a.offs[2 * o], dx = zp ? 0 : a.offs[2 * o + 1];
+          sg = fmaf(wts[o], dgp[(ti + RY + dy) * GW + (tj + RX + dx)], sg);
+        }
+        acc = fmaf(as_[n], sg, acc);
+      }
+      float* p = a.gx + ((size_t)b * C + c) * HW + (size_t)i * W + j;
+      *p += acc;
+    }
+  }
+}
+
+// BC2 (zero-pad only): per (sample, offset, row block) partial of
+//   dL/dw_o = sum_q A(q) (<dG(q+o), x(q)> + <dm(q+o), b_M>)     (o = (dy, 0): the row shift)
+struct BC2Args {
+  const float* x;
+  const float* dG;
+  const float* dmb;
+  double* dots;   // [B][k][nrb]
+  int B, C, H, W, k, nrb, rows_per;
+  float gthr;
+  int a2a;
+  int8_t offs[2 * GNCA_MAX_OFFSETS];
+};
+
+__global__ __launch_bounds__(kThreads) void gnca_b_dots(const BC2Args a) {
+  __shared__ double red[2 * NW];
+  const int tid = threadIdx.x;
+  const int per_b = a.k * a.nrb;
+  const int b = blockIdx.x / per_b, rem = blockIdx.x - b * per_b;
+  const int o = rem / a.nrb, rb = rem - o * a.nrb;
+  const int H = a.H, W = a.W, C = a.C;
+  const size_t HW = (size_t)H * W;
+  const int dy = a.offs[2 * o];
+  const int r0 = rb * a.rows_per, r1 = min(H, r0 + a.rows_per);
+  const float* xb = a.x + (size_t)b * C * HW;
+  const float* gb = a.dG + (size_t)b * C * HW;
+  double acc = 0.0;
+  for (int e = tid; e < (r1 - r0) * W; e += kThreads) {
+    const int i = r0 + e / W, j = e % W;
+    const int it = i + dy;
+    if (it < 0 || it >= H) continue;
+    if (a.a2a) {
+      float mx = -INFINITY;
+      for (int u = max(0, i - 1); u <= min(H - 1, i + 1); ++u)
+        for (int v = max(0, j - 1); v <= min(W - 1, j + 1); ++v) mx = fmaxf(mx, xb[3 * HW + (size_t)u * W + v]);
+      if (!(mx > a.gthr)) continue;
+    }
+    const size_t q = (size_t)i * W + j, t = (size_t)it * W + j;
+    float s = a.dmb[(size_t)b * HW + t];
+    for (int c = 0; c < C; ++c) s = fmaf(xb[c * HW + q], gb[c * HW + t], s);
+    acc += (double)s;
+  }
+  const double2 r = block_sum2(acc, 0.0, red);
+  if (tid == 0) a.dots[((size_t)b * a.k + o) * a.nrb + rb] = r.x;
+}
+
+// BD (zero-pad only): backward of the pooled-logit softmax (graph_augmentation.py:113-154), fp64.
+//   logit_o = qbar . kbar_o,  qbar = W_Q xbar + b_Q,  kbar_o = (W_K S_o + b_K n_o W) / HW,
+//   w = softmax(logit / (|scaling| + 1e-6)).
+// Per-sample partial gradients of W_Q, b_Q, W_K, b_K, scaling, and the per-row gx correction
+// (Q and K enter only through their spatial means, so their x-gradient is constant per row).
+struct BDArgs {
+  const float* x;
+  const float* wq;
+  const float* bq;
+  const float* wk;
+  const float* bk;
+  const float* scaling;
+  const double* dots;   // [B][k][nrb]
+  double* pq;           // [B][2*d*C + 2*d + 1]
+  float* corr;          // [B][H][C]
+  int B, C, H, W, d, k, nrb;
+  int8_t offs[2 * GNCA_MAX_OFFSETS];
+};
+
+__global__ __launch_bounds__(kThreads) void gnca_b_attn(const BDArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int C = a.C, H = a.H, W = a.W, d = a.d, k = a.k;
+  double* rs = reinterpret_cast<double*>(smem);   // [C][H]
+  double* xbar = rs + (size_t)C * H;              // [C]
+  double* qbar = xbar + C;                        // [d]
+  double* So = qbar + d;                          // [k][C]
+  double* kb = So + (size_t)k * C;                // [k][d]
+  double* L = kb + (size_t)k * d;                 // [k]
+  double* gL = L + k;                             // [k]
+  double* gqp = gL + k;                           // [d]
+  double* gkp = gqp + d;                          // [k][d]
+  double* gks = gkp + (size_t)k * d;              // [H][d]: sum of gkp over offsets valid for row
+  double* sc = gks + (size_t)H * d;               // [2]: g_scaling, HW
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t HW = (size_t)H * W;
+  const float* xb = a.x + (size_t)b * C * HW;
+  for (int cr = wave; cr < C * H; cr += NW) {
+    const int c = cr / H, r = cr - c * H;
+    double s = 0.0;
+    for (int j = lane; j < W; j += 64) s += (double)xb[c * HW + (size_t)r * W + j];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) rs[cr] = s;
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kThreads) {
+    double s = 0.0;
+    for (int r = 0; r < H; ++r) s += rs[c * H + r];
+    xbar[c] = s / (double)HW;
+  }
+  for (int e = tid; e < k * C; e += kThreads) {
+    const int o = e / C, c = e - o * C;
+    const int dy = a.offs[2 * o];
+    const int lo = dy > 0 ? 0 : -dy, hi = dy > 0 ? H - dy : H;
+    double s = 0.0;
+    for (int r = lo; r < hi; ++r) s += rs[c * H + r];
+    So[e] = s;
+  }
+  __syncthreads();
+  for (int e = tid; e < d; e += kThreads) {
+    double s = (double)a.bq[e];
+    for (int c = 0; c < C; ++c) s += (double)a.wq[e * C + c] * xbar[c];
+    qbar[e] = s;
+  }
+  for (int e = tid; e < k * d; e += kThreads) {
+    const int o = e / d, j = e - o * d;
+    const int dy = a.offs[2 * o];
+    const int lo = dy > 0 ? 0 : -dy, hi = dy > 0 ? H - dy : H;
+    const double n_o = (double)(hi > lo ? hi - lo : 0) * (double)W;
+    double s = (double)a.bk[j] * n_o;
+    for (int c = 0; c < C; ++c) s += (double)a.wk[j * C + c] * So[o * C + c];
+    kb[e] = s / (double)HW;
+  }
+  __syncthreads();
+  for (int o = tid; o < k; o += kThreads) {
+    double s = 0.0;
+    for (int j = 0; j < d; ++j) s += qbar[j] * kb[o * d + j];
+    L[o] = s;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double mx = -INFINITY;
+    for (int o = 0; o < k; ++o) mx = fmax(mx, L[o]);
+    const double sv = (double)a.scaling[0];
+    const double T = fabs(sv) + 1e-6;
+    double sum = 0.0;
+    for (int o = 0; o < k; ++o) sum += exp((L[o] - mx) / T);
+    double G = 0.0;
+    for (int o = 0; o < k; ++o) {
+      double gw = 0.0;
+      for (int r = 0; r < a.nrb; ++r) gw += a.dots[((size_t)b * k + o) * a.nrb + r];
+      gL[o] = gw;                                   // dL/dw_o for now
+      G += exp((L[o] - mx) / T) / sum * gw;
+    }
+    double gT = 0.0;
+    for (int o = 0; o < k; ++o) {
+      const double w = exp((L[o] - mx) / T) / sum;
+      const double gz = w * (gL[o] - G);
+      gL[o] = gz / T;
+      gT -= gz * (L[o] - mx) / (T * T);
+    }
+    sc[0] = gT * (sv > 0.0 ? 1.0 : (sv < 0.0 ? -1.0 : 0.0));
+  }
+  __syncthreads();
+  for (int j = tid; j < d; j += kThreads) {
+    double s = 0.0;
+    for (int o = 0; o < k; ++o) s += gL[o] * kb[o * d + j];
+    gqp[j] = s;
+  }
+  for (int e = tid; e < k * d; e += kThreads) gkp[e] = gL[e / d] * qbar[e % d];
+  __syncthreads();
+  for (int e = tid; e < H * d; e += kThreads) {
+    const int r = e / d, j = e - r * d;
+    double s = 0.0;
+    for (int o = 0; o < k; ++o) {
+      const int dy = a.offs[2 * o];
+      const int lo = dy > 0 ? 0 : -dy, hi = dy > 0 ? H - dy : H;
+      if (r >= lo && r < hi) s += gkp[o * d + j];
+    }
+    gks[e] = s;
+  }
+  double* out = a.pq + (size_t)b * (2 * d * C + 2 * d + 1);
+  for (int e = tid; e < d * C; e += kThreads) {
+    const int j = e / C, c = e - j * C;
+    out[e] = gqp[j] * xbar[c];                       // dW_Q
+    double s = 0.0;
+    for (int o = 0; o < k; ++o) s += gkp[o * d + j] * So[o * C + c];
+    out[d * C + d + e] = s / (double)HW;             // dW_K
+  }
+  for (int j = tid; j < d; j += kThreads) {
+    out[d * C + j] = gqp[j];                         // db_Q
+    double s = 0.0;
+    for (int o = 0; o < k; ++o) {
+      const int dy = a.offs[2 * o];
+      const int lo = dy > 0 ? 0 : -dy, hi = dy > 0 ? H - dy : H;
+      s += gkp[o * d + j] * (double)(hi > lo ? hi - lo : 0) * (double)W;
+    }
+    out[2 * d * C + d + j] = s / (double)HW;         // db_K
+  }
+  if (tid == 0) out[2 * d * C + 2 * d] = sc[0];      // d scaling
+  __syncthreads();
+  for (int e = tid; e < H * C; e += kThreads) {
+    const int r = e / C, c = e - r * C;
+    double s = 0.0;
+    for (int j = 0; j < d; ++j) s += (double)a.wq[j * C + c] * gqp[j] + (double)a.wk[j * C + c] * gks[r * d + j];
+    a.corr[((size_t)b * H + r) * C + c] = (float)(s / (double)HW);
+  }
+}
+
+// BE: gx[b,c,i,j] += corr[b,i,c]
+__global__ __launch_bounds__(kThreads) void gnca_b_rowcorr(float* gx, const float* corr, int B, int C,
+                                                           int H, int W) {
+  const size_t total = (size_t)B * C * H * W;
+  for (size_t e = (size_t)blockIdx.x * kThreads + threadIdx.x; e < total; e += (size_t)gridDim.x * kThreads) {
+    const size_t j = e % W, t = e / W;
+    const size_t i = t % H, t2 = t / H;
+    const size_t c = t2 % C, b = t2 / C;
+    (void)j;
+    gx[e] += corr[(b * H + i) * C + c];
+  }
+}
+
+// R: out[j] = sum_r part[r*stride + col0 + j*step], r in fixed order (deterministic)
+__global__ __launch_bounds__(kThreads) void gnca_b_reduce(const void* part, int f64, long rows, long stride,
+                                                          long col0, int ncols, int step, float* out) {
+  const int j = blockIdx.x * kThreads + threadIdx.x;
+  if (j >= ncols) return;
+  double s = 0.0;
+  const long col = col0 + (long)j * step;
+  if (f64) {
+    const double* p = reinterpret_cast<const double*>(part);
+    for (long r = 0; r < rows; ++r) s += p[r * stride + col];
+  } else {
+    const float* p = reinterpret_cast<const float*>(part);
+    for (long r = 0; r < rows; ++r) s += (double)p[r * stride + col];
+  }
+  out[j] = (float)s;
+}
+
+// ------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------
+struct BBVariant {
+  int CP, HB;
+  const void* fn;
+};
+#define GNCA_BV(cp, hb) {cp, hb, reinterpret_cast<const void*>(&gnca_b_mlp<cp, hb>)}
+static const BBVariant kBB[] = {
+    GNCA_BV(16, 128), GNCA_BV(4, 32),  GNCA_BV(8, 32),  GNCA_BV(16, 32), GNCA_BV(4, 64),
+    GNCA_BV(8, 64),   GNCA_BV(12, 64), GNCA_BV(16, 64), GNCA_BV(20, 64), GNCA_BV(24, 64),
+    GNCA_BV(28, 64),  GNCA_BV(32, 64),
+};
+#undef GNCA_BV
+
+struct BwdPlan {
+  FwdLayout F;
+  const BBVariant* bb;
+  int CP, HB, nslices;
+  bool graph, msg, zp, gn;
+  int RY, RX;
+  int TH, TW, tiles_x, tps, total_tiles, gridB;
+  size_t ldsB;
+  int band, nbands;        // BA
+  size_t ldsA;
+  int TH3, TW3, tiles_x3, tps3;   // BC
+  size_t ldsC;
+  int nrb, rows_per;       // BC2
+  size_t ldsD;
+  int npart, o_w1, o_b1, o_w2, o_wm, o_bm, nq;
+  size_t off_fwd, off_U, off_dY, off_dG, off_dmb, off_pa, off_coef, off_pb, off_dots, off_pq, off_corr, bytes;
+};
+
+static int bwd_device_cus() {
+  static std::mutex mu;
+  static std::unordered_map<int, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int cus = 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  cache[dev] = cus;
+  return cus;
+}
+
+static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
+  if (!d || !fwd_layout(d, &P->F)) return false;
+  const int C = d->C, Hd = d->hidden, H = d->H, W = d->W;
+  P->CP = (C + 3) & ~3;
+  P->graph = (d->flags & GNCA_GRAPH) != 0;
+  P->msg = P->graph && P->F.k > 0 && d->message_gain != 0.f;
+  P->zp = (d->flags & GNCA_ZERO_PAD_SHIFT) != 0;
+  P->gn = (d->flags & GNCA_USE_GROUPNORM) != 0;
+  // hidden slice width: the largest compiled HB <= 128 for this CP that is not much wider than Hd
+  P->bb = nullptr;
+  for (const BBVariant& v : kBB) {
+    if (v.CP != P->CP) continue;
+    if (!P->bb) { P->bb = &v; continue; }
+    const int cur = P->bb->HB;
+    const bool cur_fits = cur >= Hd, v_fits = v.HB >= Hd;
+    if (v_fits && (!cur_fits || v.HB < cur)) P->bb = &v;
+    else if (!v_fits && !cur_fits && v.HB > cur) P->bb = &v;
+  }
+  if (!P->bb) return false;
+  P->HB = P->bb->HB;
+  P->nslices = (Hd + P->HB - 1) / P->HB;
+  int ry = 1, rx = 1;
+  if (P->msg)
+    for (int o = 0; o < P->F.k; ++o) {
+      ry = std::max(ry, std::abs((int)d->offsets[2 * o]));
+      if (!P->zp) rx = std::max(rx, std::abs((int)d->offsets[2 * o + 1]));
+    }
+  P->RY = ry;
+  P->RX = rx;
+  // BB tile: fewest padded cells + staged halo within 160 KB LDS
+  static const int ths[] = {4, 8, 16};
+  static const int tws[] = {8, 16, 24, 32};
+  double best = 1e300;
+  P->TH = 0;
+  for (int th : ths)
+    for (int tw : tws) {
+      if ((th * tw) % 64) continue;
+      const BBLayout L = bb_layout(P->CP, P->HB, th, tw, ry, rx, P->F.k);
+      const size_t bytes = (size_t)L.total * 4;
+      if (bytes > 160 * 1024) continue;
+      const long tx = (W + tw - 1) / tw, ty = (H + th - 1) / th;
+      const double cost = (double)tx * ty * th * tw + 0.01 * tx * ty * L.RH * L.RW * P->CP + 30.0 * tx * ty;
+      if (cost < best) { best = cost; P->TH = th; P->TW = tw; P->ldsB = bytes; }
+    }
+  if (!P->TH) return false;
+  P->tiles_x = (W + P->TW - 1) / P->TW;
+  P->tps = P->tiles_x * ((H + P->TH - 1) / P->TH);
+  P->total_tiles = P->tps * d->B;
+  P->gridB = std::min(bwd_device_cus(), P->total_tiles);
+  if (P->gridB < 1) P->gridB = 1;
+  // BA bands (as the forward K2)
+  {
+    long rows = (H + 7) / 8;
+    const long cap = (48L * 1024 / 4 / W - 2) / 2;
+    if (rows > cap) rows = cap;
+    if (rows < 1) rows = 1;
+    P->band = (int)rows;
+    P->nbands = (H + P->band - 1) / P->band;
+    P->ldsA = (size_t)(2 * P->band + 2) * W * 4;
+    if (P->ldsA > 64 * 1024) return false;
+  }
+  // BC tiles
+  P->TH3 = 16;
+  P->TW3 = 16;
+  P->tiles_x3 = (W + P->TW3 - 1) / P->TW3;
+  P->tps3 = P->tiles_x3 * ((H + P->TH3 - 1) / P->TH3);
+  {
+    const int PA = (P->TH3 + 2) * (P->TW3 + 2);
+    const int GA = (P->TH3 + 2 * ry) * (P->TW3 + 2 * (P->zp ? 0 : rx));
+    P->ldsC = (size_t)(3 * PA + GA + P->TH3 * P->TW3 + std::max(P->F.k, 1) + PA) * 4;
+  }
+  P->rows_per = std::max(1, (int)((4096 + W - 1) / W));
+  P->nrb = (H + P->rows_per - 1) / P->rows_per;
+  const int dm = std::max(d->d_model, 1), k = std::max(P->F.k, 1);
+  P->ldsD = ((size_t)C * H + C + dm + (size_t)k * C + (size_t)k * dm + 2 * k + dm + (size_t)k * dm +
+             (size_t)H * dm + 2) * sizeof(double);
+  if (P->msg && P->zp && P->ldsD > 64 * 1024) return false;
+  P->o_w1 = 0;
+  P->o_b1 = Hd * 3 * C;
+  P->o_w2 = P->o_b1 + Hd;
+  P->o_wm = P->o_w2 + C * Hd;
+  P->o_bm = P->o_wm + C * C;
+  P->npart = P->o_bm + C;
+  P->nq = 2 * dm * C + 2 * dm + 1;
+  const size_t n = (size_t)d->B * C * H * W, hw = (size_t)d->B * H * W;
+  size_t o = 0;
+  auto carve = [&o](size_t bytes) { size_t at = o; o += (bytes + 255) & ~(size_t)255; return at; };
+  P->off_fwd = carve(P->F.ws_bytes);
+  P->off_U = carve(n * 4);
+  P->off_dY = carve(3 * n * 4);
+  P->off_dG = carve(P->msg ? n * 4 : 0);
+  P->off_dmb = carve(P->msg && P->zp ? hw * 4 : 0);
+  P->off_pa = carve((size_t)d->B * P->nbands * (2 + 2 * C) * 8);
+  P->off_coef = carve((size_t)d->B * 4 * 4);
+  P->off_pb = carve((size_t)P->gridB * NW * P->npart * 4);
+  const bool att = P->msg && P->zp;
+  P->off_dots = carve(att ? (size_t)d->B * P->F.k * P->nrb * 8 : 0);
+  P->off_pq = carve(att ? (size_t)d->B * P->nq * 8 : 0);
+  P->off_corr = carve(att ? (size_t)d->B * H * C * 4 : 0);
+  P->bytes = o;
+  return true;
+}
+
+static int bwd_check() {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_last_hip = (int)e;
+    return GNCA_ERR_HIP;
+  }
+  return GNCA_OK;
+}
+
+static int reduce_into(const void* part, bool f64, long rows, long stride, long col0, int ncols,
+                       int step, float* out, hipStream_t st) {
+  if (!out || ncols <= 0) return GNCA_OK;
+  hipLaunchKernelGGL(gnca_b_reduce, dim3((ncols + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
+                     part, f64 ? 1 : 0, rows, stride, col0, ncols, step, out);
+  return bwd_check();
+}
+
+static int zero_grad(float* p, size_t n, hipStream_t st) {
+  if (!p || n == 0) return GNCA_OK;
+  return hipMemsetAsync(p, 0, n * sizeof(float), st) == hipSuccess ? GNCA_OK : GNCA_ERR_HIP;
+}
+
+}  // namespace
+}  // namespace gnca
+
+using namespace gnca;
+
+extern "C" {
+
+size_t gnca_bwd_workspace_bytes(const gnca_step_desc* desc) {
+  BwdPlan P;
+  if (!bwd_plan(desc, &P)) return 0;
+  return P.bytes;
+}
+
+int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
+                      const void* fire, const float* gy, float* gx, const gnca_grads* grads,
+                      void* ws, size_t ws_bytes, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (!desc || !w || !x || !gy || !gx || !grads) return GNCA_ERR_INVALID;
+  if (gx == x || gx == gy) return GNCA_ERR_INVALID;
+  gnca_step_desc d = *desc;
+  d.flags &= ~GNCA_ATTENTION;
+  BwdPlan P;
+  if (!bwd_plan(&d, &P)) return GNCA_ERR_INVALID;
+  if (!ws || ws_bytes < P.bytes) return GNCA_ERR_WORKSPACE;
+  if (P.gn && (!w->gn_weight || !w->gn_bias)) return GNCA_ERR_INVALID;
+  if (P.msg && (!w->wm || !w->bm)) return GNCA_ERR_INVALID;
+  if (P.msg && P.zp && (!w->wq || !w->bq || !w->wk || !w->bk || !w->scaling)) return GNCA_ERR_INVALID;
+  char* wsb = reinterpret_cast<char*>(ws);
+  const int B = d.B, C = d.C, H = d.H, W = d.W, Hd = d.hidden;
+  const size_t HW = (size_t)H * W;
+  int rc;
+  // F: recompute the forward's dx / GroupNorm partials / offset weights (gx is a dummy x_out:
+  // phase K2, the only writer of x_out, is not run)
+  if ((rc = gnca_step_phases_f32(&d, w, x, gx, fire, nullptr, wsb + P.off_fwd, P.F.ws_bytes, stream,
+                                 GNCA_PHASE_K0 | GNCA_PHASE_K1)) != GNCA_OK)
+    return rc;
+  const float* dx = reinterpret_cast<const float*>(wsb + P.off_fwd + P.F.off_dx);
+  const double* stats = reinterpret_cast<const double*>(wsb + P.off_fwd + P.F.off_stats);
+  const float* offw = (P.msg && P.zp) ? reinterpret_cast<const float*>(wsb + P.off_fwd + P.F.off_offw) : nullptr;
+  float* U = reinterpret_cast<float*>(wsb + P.off_U);
+  float* dY = reinterpret_cast<float*>(wsb + P.off_dY);
+  float* dG = reinterpret_cast<float*>(wsb + P.off_dG);
+  float* dmb = (P.msg && P.zp) ? reinterpret_cast<float*>(wsb + P.off_dmb) : nullptr;
+  double* pa = reinterpret_cast<double*>(wsb + P.off_pa);
+  float* coef = reinterpret_cast<float*>(wsb + P.off_coef);
+  float* pb = reinterpret_cast<float*>(wsb + P.off_pb);
+  // BA
+  {
+    BAArgs a;
+    memset(&a, 0, sizeof(a));
+    a.x = x; a.dx = dx; a.gy = gy; a.gamma = w->gn_weight; a.beta = w->gn_bias; a.stats = stats;
+    a.gx = gx; a.U = U; a.part = pa;
+    a.B = B; a.C = C; a.H = H; a.W = W; a.tps = P.F.tps; a.band = P.band; a.nbands = P.nbands;
+    a.gain = d.update_gain; a.thr = d.alpha_thr; a.eps = d.gn_eps; a.use_gn = P.gn ? 1 : 0;
+    hipLaunchKernelGGL(gnca_b_gnprep, dim3(B * P.nbands), dim3(kThreads), P.ldsA, st, a);
+    if ((rc = bwd_check()) != GNCA_OK) return rc;
+  }
+  // BS
+  hipLaunchKernelGGL(gnca_b_coef, dim3((B + kThreads - 1) / kThreads), dim3(kThreads), 0, st, stats,
+                     (const double*)pa, coef, B, C, (int)HW, P.F.tps, P.nbands, d.gn_eps, P.gn ? 1 : 0);
+  if ((rc = bwd_check()) != GNCA_OK) return rc;
+  // BB, one launch per hidden slice
+  {
+    BBArgs a;
+    memset(&a, 0, sizeof(a));
+    a.x = x; a.U = U; a.dx = dx; a.coef = coef; a.fire = fire;
+    a.perc = w->perception; a.w1 = w->w1; a.b1 = w->b1; a.w2 = w->w2; a.wm = w->wm; a.bm = w->bm;
+    a.offw = offw; a.dY = dY; a.dG = dG; a.dmb = dmb; a.part = pb;
+    a.seed = d.rng_seed; a.rng_step = d.rng_step; a.sample_base = d.sample_base;
+    a.B = B; a.C = C; a.H = H; a.W = W; a.hidden = Hd; a.k = P.msg ? P.F.k : 0;
+    a.RY = P.RY; a.RX = P.RX; a.TH = P.TH; a.TW = P.TW; a.tiles_x = P.tiles_x; a.tps = P.tps;
+    a.total_tiles = P.total_tiles; a.fire_mode = d.fire_mode;
+    a.npart = P.npart; a.o_w1 = P.o_w1; a.o_b1 = P.o_b1; a.o_w2 = P.o_w2; a.o_wm = P.o_wm; a.o_bm = P.o_bm;
+    a.fire_rate = d.fire_rate; a.alpha_thr = d.alpha_thr; a.graph_alpha_thr = d.graph_alpha_thr;
+    a.message_gain = d.message_gain;
+    a.uniform_w = P.F.k > 0 ? (float)(1.0 / (double)P.F.k) : 0.f;
+    a.flags = d.flags & (GNCA_ZERO_PAD_SHIFT | GNCA_ALIVE_TO_ALIVE | GNCA_HIDDEN_ONLY);
+    if (P.msg) a.flags |= kMsg;
+    if (P.gn) a.flags |= kGN;
+    const int RW = P.TW + 2 * P.RX;
+    for (int o = 0; o < a.k; ++o) a.odl[o] = d.offsets[2 * o] * RW + (P.zp ? 0 : d.offsets[2 * o + 1]);
+    (void)hipFuncSetAttribute(P.bb->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.ldsB);
+    for (int s = 0; s < P.nslices; ++s) {
+      a.h0 = s * P.HB;
+      a.flags = (a.flags & ~kFirst) | (s == 0 ? kFirst : 0u);
+      void* args[] = {&a};
+      const hipError_t e = hipLaunchKernel(P.bb->fn, dim3(P.gridB), dim3(kThreads), args, P.ldsB, st);
+      if (e != hipSuccess) { g_last_hip = (int)e; return GNCA_ERR_HIP; }
+      if ((rc = bwd_check()) != GNCA_OK) return rc;
+    }
+  }
+  // BC
+  {
+    BCArgs a;
+    memset(&a, 0, sizeof(a));
+    a.dY = dY; a.dG = dG; a.x = x; a.perc = w->perception; a.offw = offw; a.gx = gx;
+    a.B = B; a.C = C; a.H = H; a.W = W; a.k = P.msg ? P.F.k : 0;
+    a.TH = P.TH3; a.TW = P.TW3; a.tiles_x = P.tiles_x3; a.tps = P.tps3;
+    a.RY = P.RY; a.RX = P.zp ? 0 : P.RX;
+    a.graph_alpha_thr = d.graph_alpha_thr;
+    a.uniform_w = P.F.k > 0 ? (float)(1.0 / (double)P.F.k) : 0.f;
+    a.flags = (d.flags & (GNCA_ZERO_PAD_SHIFT | GNCA_ALIVE_TO_ALIVE)) | (P.msg ? kMsg : 0u);
+    for (int o = 0; o < 2 * a.k; ++o) a.offs[o] = d.offsets[o];
+    hipLaunchKernelGGL(gnca_b_adjoint, dim3(B * P.tps3), dim3(kThreads), P.ldsC, st, a);
+    if ((rc = bwd_check()) != GNCA_OK) return rc;
+  }
+  const long rowsB = (long)P.gridB * NW;
+  if ((rc = reduce_into(pb, false, rowsB, P.npart, P.o_w1, Hd * 3 * C, 1, grads->w1, st)) ||
+      (rc = reduce_into(pb, false, rowsB, P.npart, P.o_b1, Hd, 1, grads->b1, st)) ||
+      (rc = reduce_into(pb, false, rowsB, P.npart, P.o_w2, C * Hd, 1, grads->w2, st)))
+    return rc;
+  if (P.gn) {
+    if ((rc = reduce_into(pa, true, (long)B * P.nbands, 2 + 2 * C, 2, C, 2, grads->gn_weight, st)) ||
+        (rc = reduce_into(pa, true, (long)B * P.nbands, 2 + 2 * C, 3, C, 2, grads->gn_bias, st)))
+      return rc;
+  }
+  if (!P.graph) return GNCA_OK;
+  if ((rc = reduce_into(pb, false, rowsB, P.npart, P.o_wm, C * C, 1, grads->wm, st)) ||
+      (rc = reduce_into(pb, false, rowsB, P.npart, P.o_bm, C, 1, grads->bm, st)))
+    return rc;
+  const int dmod = std::max(d.d_model, 1);
+  if (!(P.msg && P.zp)) {  // torus (or no message): the offset weights are constants
+    if ((rc = zero_grad(grads->wq, (size_t)dmod * C, st)) || (rc = zero_grad(grads->bq, dmod, st)) ||
+        (rc = zero_grad(grads->wk, (size_t)dmod * C, st)) || (rc = zero_grad(grads->bk, dmod, st)) ||
+        (rc = zero_grad(grads->scaling, 1, st)))
+      return rc;
+    return GNCA_OK;
+  }
+  double* dots = reinterpret_cast<double*>(wsb + P.off_dots);
+  double* pq = reinterpret_cast<double*>(wsb + P.off_pq);
+  float* corr = reinterpret_cast<float*>(wsb + P.off_corr);
+  {
+    BC2Args a;
+    memset(&a, 0, sizeof(a));
+    a.x = x; a.dG = dG; a.dmb = dmb; a.dots = dots;
+    a.B = B; a.C = C; a.H = H; a.W = W; a.k = P.F.k; a.nrb = P.nrb; a.rows_per = P.rows_per;
+    a.gthr = d.graph_alpha_thr; a.a2a = (d.flags & GNCA_ALIVE_TO_ALIVE) ? 1 : 0;
+    for (int o = 0; o < 2 * P.F.k; ++o) a.offs[o] = d.offsets[o];
+    hipLaunchKernelGGL(gnca_b_dots, dim3(B * P.F.k * P.nrb), dim3(kThreads), 0, st, a);
+    if ((rc = bwd_check()) != GNCA_OK) return rc;
+  }
+  {
+    BDArgs a;
+    memset(&a, 0, sizeof(a));
+    a.x = x; a.wq = w->wq; a.bq = w->bq; a.wk = w->wk; a.bk = w->bk; a.scaling = w->scaling;
+    a.dots = dots; a.pq = pq; a.corr = corr;
+    a.B = B; a.C = C; a.H = H; a.W = W; a.d = d.d_model; a.k = P.F.k; a.nrb = P.nrb;
+    for (int o = 0; o < 2 * P.F.k; ++o) a.offs[o] = d.offsets[o];
+    hipLaunchKernelGGL(gnca_b_attn, dim3(B), dim3(kThreads), P.ldsD, st, a);
+    if ((rc = bwd_check()) != GNCA_OK) return rc;
+  }
+  {
+    const size_t total = (size_t)B * C * HW;
+    size_t blocks = (total + kThreads - 1) / kThreads;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(gnca_b_rowcorr, dim3((unsigned)blocks), dim3(kThreads), 0, st, gx, (const float*)corr,
+                       B, C, H, W);
+    if ((rc = bwd_check()) != GNCA_OK) return rc;
+  }
+  const int dq = d.d_model;
+  if ((rc = reduce_into(pq, true, B, P.nq, 0, dq * C, 1, grads->wq, st)) ||
+      (rc = reduce_into(pq, true, B, P.nq, dq * C, dq, 1, grads->bq, st)) ||
+      (rc = reduce_into(pq, true, B, P.nq, dq * C + dq, dq * C, 1, grads->wk, st)) ||
+      (rc = reduce_into(pq, true, B, P.nq, 2 * dq * C + dq, dq, 1, grads->bk, st)) ||
+      (rc = reduce_into(pq, true, B, P.nq, 2 * dq * C + 2 * dq, 1, 1, grads->scaling, st)))
+    return rc;
+  return GNCA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+// gnca_device.h — device helpers shared by the forward (gnca_step.hip) and backward
+// (gnca_bwd.hip) translation units of libgnca.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "gnca.h"
+
+namespace gnca {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ int wrapi(int v, int n) {
+  v %= n;
+  return v < 0 ? v + n : v;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Counter-based fire RNG (the build's definition; oracle/nca_oracle.py:hash_uniform).
+__device__ __forceinline__ float hash_uniform(uint64_t seed, int64_t step, uint64_t sample,
+                                              uint64_t cell) {
+  const uint64_t k = mix64(seed + 0x9E3779B97F4A7C15ull * (uint64_t)(uint32_t)(step + 1));
+  const uint64_t key = mix64(k ^ (sample << 32) ^ cell);
+  return (float)(key >> 40) * (1.0f / 16777216.0f);
+}
+
+// The fire predicate of one cell (ncagraph.py:144-146), for every GNCA_FIRE_* mode.
+__device__ __forceinline__ bool fire_at(int mode, const void* fire, float rate, uint64_t seed,
+                                        int64_t step, int64_t sample_base, int b, size_t HW,
+                                        size_t cell) {
+  if (mode == GNCA_FIRE_RAND_F32) return reinterpret_cast<const float*>(fire)[(size_t)b * HW + cell] <= rate;
+  if (mode == GNCA_FIRE_MASK_U8) return reinterpret_cast<const uint8_t*>(fire)[(size_t)b * HW + cell] != 0;
+  if (mode == GNCA_FIRE_HASH) return hash_uniform(seed, step, (uint64_t)(sample_base + b), cell) <= rate;
+  return true;
+}
+
+__host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
+__host__ __device__ inline int odd4(int v) {  // round up to 4*odd: conflict-free 16-lane b128
+  v = r4(v);
+  return ((v >> 2) & 1) ? v : v + 4;
+}
+
+// Where the forward keeps its intermediates in the step workspace (gnca_step.hip:make_plan);
+// the backward recomputes them there.
+struct FwdLayout {
+  size_t ws_bytes, off_dx, off_stats, off_offw;
+  int tps, k;
+  bool graph_on, need_k0;
+};
+bool fwd_layout(const gnca_step_desc* d, FwdLayout* out);
+
+// hipError_t of the last failed launch on this thread (gnca_last_hip_error)
+extern thread_local int g_last_hip;
+
+}  // namespace gnca

@@ -28,23 +28,13 @@
 // so each lane computes its own perception features.  GEMM1's accumulator rows (hidden 4g+r of
 // tile m) are exactly the B operand of GEMM2 DL = W2 H at k-step (m, r) — no data movement.
 
-#include <hip/hip_runtime.h>
-
-#include <math.h>
-#include <stdint.h>
-#include <string.h>
-
 #include <mutex>
 #include <type_traits>
 #include <unordered_map>
 
-#include "gnca.h"
+#include "gnca_device.h"
 
 namespace gnca {
-
-typedef float f4 __attribute__((ext_vector_type(4)));
-
-constexpr int kThreads = 256;
 
 // Measurement-only ablation switches (tools/ablate.py builds variants with -DGNCA_ABLATE=<bits>;
 // the product library is always built with 0).  Outputs are wrong in an ablated build.
@@ -62,25 +52,6 @@ constexpr uint32_t kGraphOn = 1u << 17;   // internal K1 flag: gather + message 
 
 __device__ float g_zero[4];  // LDS-DMA source for off-image cells (zero-initialised)
 
-__device__ __forceinline__ int wrapi(int v, int n) {
-  v %= n;
-  return v < 0 ? v + n : v;
-}
-
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-// Counter-based fire RNG (the build's definition; oracle/nca_oracle.py:hash_uniform).
-__device__ __forceinline__ float hash_uniform(uint64_t seed, int64_t step, uint64_t sample,
-                                              uint64_t cell) {
-  const uint64_t k = mix64(seed + 0x9E3779B97F4A7C15ull * (uint64_t)(uint32_t)(step + 1));
-  const uint64_t key = mix64(k ^ (sample << 32) ^ cell);
-  return (float)(key >> 40) * (1.0f / 16777216.0f);
-}
-
 // ------------------------------------------------------------------------------------------
 // LDS layout of K1 (floats; every region starts on a 16-byte boundary)
 // ------------------------------------------------------------------------------------------
@@ -89,11 +60,6 @@ struct K1Layout {
   int RH, RW, PSTR, NI, NIA, ALW;
 };
 
-__host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
-__host__ __device__ inline int odd4(int v) {  // round up to 4*odd: conflict-free 16-lane b128
-  v = r4(v);
-  return ((v >> 2) & 1) ? v : v + 4;
-}
 // W1 fragments stay in LDS (read as 16-byte fragments every group: LDS reads cost no VALU, and
 // keeping them out of VGPRs removes spills and leaves room to keep loads in flight)
 __host__ __device__ constexpr bool w1_in_regs(int, int) { return false; }
@@ -1111,6 +1077,20 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
     const size_t k0 = ((size_t)d->C * d->H + d->C + d->d_model + P->k) * sizeof(double);
     if (k0 > 64 * 1024) return false;
   }
+  return true;
+}
+
+bool fwd_layout(const gnca_step_desc* d, FwdLayout* out) {
+  Plan P;
+  if (!make_plan(d, false, &P)) return false;
+  out->ws_bytes = P.ws_bytes;
+  out->off_dx = P.off_dx;
+  out->off_stats = P.off_stats;
+  out->off_offw = P.off_offw;
+  out->tps = P.tps;
+  out->k = P.k;
+  out->graph_on = P.graph_on;
+  out->need_k0 = P.need_k0;
   return true;
 }
 

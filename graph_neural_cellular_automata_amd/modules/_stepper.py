@@ -9,22 +9,41 @@ from .. import step as S
 
 
 class _StepFn(torch.autograd.Function):
-    """The HIP step as an autograd node.  Forward values come from libgnca.so.  The BPTT
-    backward kernel is SURVEY.md §8f rank 1 ("next") and is not built yet: asking for a gradient
-    through this node raises instead of silently routing through another implementation."""
+    """The HIP step as an autograd node (BPTT through the trainers' rollouts).
+
+    Forward: ``gnca_step_f32``.  Backward: ``gnca_step_bwd_f32``, which recomputes the step's
+    intermediates from the saved input state, so a rollout keeps only its states alive (as the
+    reference's autograd graph would, minus the per-op activations).  Gradients follow the
+    reference's graph of tensors: masks are constants, the perception weight is frozen,
+    ``gate_mlp`` is never used (None), and the graph parameters get None when no offsets were
+    drawn (``graph_augmentation.py:141-147`` returns zeros without touching them)."""
 
     @staticmethod
-    def forward(ctx, x, desc, weights, fire, want_attn, *params):
+    def forward(ctx, x, desc, weights, keep, fire, want_attn, names, *params):
         out, attn = S.step(desc, weights, x, fire=fire, want_attention=want_attn)
         if attn is not None:
             ctx.mark_non_differentiable(attn)
+        ctx.save_for_backward(x)
+        ctx.desc, ctx.weights, ctx.keep, ctx.fire, ctx.names = desc, weights, keep, fire, names
+        ctx.params = params
         return out, attn
 
     @staticmethod
-    def backward(ctx, *grads):
-        raise NotImplementedError(
-            "graph_neural_cellular_automata_amd: backward through the NCA step (BPTT) is not "
-            "implemented yet; run rollouts under torch.no_grad()")
+    def backward(ctx, gout, gattn):
+        (x,) = ctx.saved_tensors
+        desc = ctx.desc
+        no_graph_use = (desc.flags & L.GRAPH) and desc.num_offsets == 0
+        need = ctx.needs_input_grad[7:]
+        want = {}
+        for name, p, nd in zip(ctx.names, ctx.params, need):
+            if not nd or name not in S.GRAD_FIELDS:
+                continue
+            if no_graph_use and name.startswith("graph."):
+                continue
+            want[name] = p
+        gx, grads = S.step_backward(desc, ctx.weights, x, gout.contiguous(), fire=ctx.fire, want=want)
+        pgrads = [grads.get(n) for n in ctx.names]
+        return (gx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, *pgrads)
 
 
 def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen, message_gain,
@@ -66,10 +85,11 @@ def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen,
                        graph_alpha_thr=graph_thr, message_gain=message_gain,
                        fire_rate=fire_rate, fire_mode=fire_mode, gn_eps=eps)
     w, keep = S.make_weights(tensors)
-    params = [p for p in model.parameters() if p.requires_grad]
-    if torch.is_grad_enabled() and (x.requires_grad or params):
-        out, attn = _StepFn.apply(x, desc, w, fire, return_attention, *params)
+    named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+    if torch.is_grad_enabled() and (x.requires_grad or named):
+        names = tuple(n for n, _ in named)
+        params = [p for _, p in named]
+        out, attn = _StepFn.apply(x, desc, w, keep, fire, return_attention, names, *params)
     else:
         out, attn = S.step(desc, w, x, fire=fire, want_attention=return_attention)
-    del keep
     return out, attn

@@ -144,3 +144,40 @@ def rollout(desc, weights, x, steps: int, offsets_per_step: list):
                               ws.numel(), stream_ptr(x.device))
     L.check(rc, "gnca_rollout_f32")
     return out
+
+
+# parameter name (state_dict suffix) -> gnca_grads field
+GRAD_FIELDS = {
+    "update_net.0.weight": "w1", "update_net.0.bias": "b1", "update_net.2.weight": "w2",
+    "norm.weight": "gn_weight", "norm.bias": "gn_bias",
+    "graph.query_proj.weight": "wq", "graph.query_proj.bias": "bq",
+    "graph.key_proj.weight": "wk", "graph.key_proj.bias": "bk",
+    "graph.msg_proj.weight": "wm", "graph.msg_proj.bias": "bm", "graph.scaling": "scaling",
+}
+
+
+def step_backward(desc, weights, x, gy, fire=None, want: dict | None = None):
+    """Vector-Jacobian product of one step (gnca_step_bwd_f32).
+
+    ``want`` maps state_dict names (GRAD_FIELDS keys) to the parameter tensors whose gradients
+    are wanted; returns ``(gx, {name: grad})`` with grads shaped like the parameters."""
+    lib = L.load()
+    gy = _dev_f32(gy, "grad_output")
+    gx = torch.empty_like(x)
+    g = L.Grads()
+    out = {}
+    for name, p in (want or {}).items():
+        t = torch.empty(p.shape, dtype=torch.float32, device=x.device)
+        out[name] = t
+        setattr(g, GRAD_FIELDS[name], t.data_ptr())
+    n = lib.gnca_bwd_workspace_bytes(ctypes.byref(desc))
+    if n == 0:
+        raise L.GncaError(
+            f"unsupported step shape for the backward: B={desc.B} C={desc.C} H={desc.H} "
+            f"W={desc.W} hidden={desc.hidden}")
+    ws = torch.empty(n, dtype=torch.uint8, device=x.device)
+    rc = lib.gnca_step_bwd_f32(ctypes.byref(desc), ctypes.byref(weights), x.data_ptr(), _ptr(fire),
+                               gy.data_ptr(), gx.data_ptr(), ctypes.byref(g), ws.data_ptr(),
+                               ws.numel(), stream_ptr(x.device))
+    L.check(rc, "gnca_step_bwd_f32")
+    return gx, out

@@ -26,6 +26,10 @@
  *   gnca_rollout_f32     the rollout loops that call the step once per CA step, e.g.
  *                        src/training/train_graph_augmented_nca.py:305-321,
  *                        src/testing/test_graph_augmented_regeneration.py:183-194
+ *   gnca_step_bwd_f32    torch autograd's backward through NeuralCAGraph.forward /
+ *                        NeuralCA.forward, i.e. the per-step part of the trainers'
+ *                        loss.backward() (BPTT): src/training/train_graph_augmented_nca.py:369,
+ *                        src/training/train_intermediate_loss.py (same loop)
  */
 #ifndef GNCA_H
 #define GNCA_H
@@ -37,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GNCA_ABI_VERSION 1
+#define GNCA_ABI_VERSION 2
 #define GNCA_MAX_OFFSETS 128   /* >= (2r+1)^2-9 for r <= 5 (112) */
 
 /* gnca_step_desc.flags */
@@ -151,6 +155,41 @@ int gnca_perceive_f32(int32_t B, int32_t C, int32_t H, int32_t W, const float* w
 int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
                      const int8_t* offsets, const float* x, float* x_final, float* scratch,
                      void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Backward (BPTT).  Gradients of one step, written into caller buffers (overwritten, not
+ * accumulated), in the reference's parameter layouts.  A NULL pointer skips that gradient's
+ * write (e.g. gn_weight/gn_bias without GNCA_USE_GROUPNORM, the graph fields for NeuralCA).
+ * -------------------------------------------------------------------------------------------*/
+typedef struct gnca_grads {
+  float* w1;          /* d update_net.0.weight  [hidden,3C,1,1] */
+  float* b1;          /* d update_net.0.bias    [hidden]        */
+  float* w2;          /* d update_net.2.weight  [C,hidden,1,1]  */
+  float* gn_weight;   /* d norm.weight          [C]             */
+  float* gn_bias;     /* d norm.bias            [C]             */
+  float* wq;          /* d graph.query_proj.weight [d,C,1,1]    */
+  float* bq;          /* d graph.query_proj.bias   [d]          */
+  float* wk;          /* d graph.key_proj.weight   [d,C,1,1]    */
+  float* bk;          /* d graph.key_proj.bias     [d]          */
+  float* wm;          /* d graph.msg_proj.weight   [C,C,1,1]    */
+  float* bm;          /* d graph.msg_proj.bias     [C]          */
+  float* scaling;     /* d graph.scaling           []           */
+} gnca_grads;
+
+/* Bytes of device workspace gnca_step_bwd_f32 needs for `desc` (0 on invalid desc). */
+size_t gnca_bwd_workspace_bytes(const gnca_step_desc* desc);
+
+/*
+ * Vector-Jacobian product of one step: given the step input x (and the same desc, weights and
+ * fire input as the forward call) and gy = dL/d x_out, write gx = dL/dx and the parameter
+ * gradients.  The step's forward intermediates are recomputed (nothing is saved by the forward).
+ * The alive / fire masks are constants, the perception weight is frozen (no gradient), as in the
+ * reference's autograd graph.  In torus mode the offset weights are exactly uniform, so the
+ * query/key/scaling gradients are exactly zero.  gx must not alias x or gy.
+ */
+int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
+                      const void* fire, const float* gy, float* gx, const gnca_grads* grads,
+                      void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

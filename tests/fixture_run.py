@@ -40,7 +40,7 @@ def desc_for(case, B, H, W, chosen, fire_mode, attention=False, **over):
     kw = dict(B=B, C=m["C"], H=H, W=W, hidden=m["Hd"], d_model=m["d"],
               offsets=chosen if m["graph"] else [], flags=flags, update_gain=m["update_gain"],
               alpha_thr=m["alpha_thr"], message_gain=m["message_gain"],
-              fire_rate=m["fire_rate"], fire_mode=fire_mode)
+              fire_rate=m.get("fire_rate", 1.0), fire_mode=fire_mode)
     kw.update(over)
     return S.make_desc(**kw)
 

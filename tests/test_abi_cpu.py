@@ -45,9 +45,13 @@ def test_struct_layout_matches_header(tmp_path):
     """Compile a C probe against gnca.h and compare offsetof/sizeof with the ctypes mirrors."""
     fields_d = [f for f, _ in L.StepDesc._fields_]
     fields_w = [f for f, _ in L.Weights._fields_]
+    fields_g = [f for f, _ in L.Grads._fields_]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gnca.h"', 'int main(void){']
     lines.append('printf("desc %zu\\n", sizeof(gnca_step_desc));')
     lines.append('printf("weights %zu\\n", sizeof(gnca_weights));')
+    lines.append('printf("grads %zu\\n", sizeof(gnca_grads));')
+    for f in fields_g:
+        lines.append(f'printf("g.{f} %zu\\n", offsetof(gnca_grads, {f}));')
     for f in fields_d:
         lines.append(f'printf("d.{f} %zu\\n", offsetof(gnca_step_desc, {f}));')
     for f in fields_w:
@@ -64,6 +68,9 @@ def test_struct_layout_matches_header(tmp_path):
         assert int(got[f"d.{f}"]) == getattr(L.StepDesc, f).offset, f
     for f in fields_w:
         assert int(got[f"w.{f}"]) == getattr(L.Weights, f).offset, f
+    assert int(got["grads"]) == ctypes.sizeof(L.Grads)
+    for f in fields_g:
+        assert int(got[f"g.{f}"]) == getattr(L.Grads, f).offset, f
 
 
 def _desc(**kw):
@@ -97,4 +104,22 @@ def test_step_rejects_bad_args_without_touching_gpu(lib):
     rc = lib.gnca_step_f32(ctypes.byref(d), ctypes.byref(w), None, None, None, None, None, 0, None)
     assert rc == -1
     rc = lib.gnca_rollout_f32(ctypes.byref(d), ctypes.byref(w), 3, None, None, None, None, None, 0, None)
+    assert rc == -1
+
+
+def test_bwd_workspace_bytes_host_only(lib):
+    d = _desc()
+    n = lib.gnca_bwd_workspace_bytes(ctypes.byref(d))
+    # forward workspace + U + dY(3C) + dG at least
+    assert n >= lib.gnca_workspace_bytes(ctypes.byref(d)) + 5 * 4 * 16 * 72 * 72 * 4
+    for bad in (dict(C=3), dict(C=36), dict(hidden=512), dict(B=0)):
+        assert lib.gnca_bwd_workspace_bytes(ctypes.byref(_desc(**bad))) == 0
+
+
+def test_bwd_rejects_bad_args_without_touching_gpu(lib):
+    d = _desc()
+    w = L.Weights()
+    g = L.Grads()
+    rc = lib.gnca_step_bwd_f32(ctypes.byref(d), ctypes.byref(w), None, None, None, None, ctypes.byref(g),
+                               None, 0, None)
     assert rc == -1

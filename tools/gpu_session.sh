@@ -20,6 +20,7 @@ for s in "$@"; do
   case $s in
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     testsall) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    grad) run pytest_grad 600 python -m pytest tests/test_gpu_grad.py -m gpu -q -p no:cacheprovider ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 96 --warmup 8 ;;
     benchq) run bench 600 python bench.py --steps 24 --warmup 4 --no-cpu ;;
