@@ -106,7 +106,7 @@ def load(path: str = LIB_PATH):
     lib.gnca_bwd_workspace_bytes.argtypes = [ctypes.POINTER(StepDesc)]
     lib.gnca_step_bwd_f32.restype = ctypes.c_int
     lib.gnca_step_bwd_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights), vp, vp, vp,
-                                      vp, ctypes.POINTER(Grads), vp, sz, vp]
+                                      vp, ctypes.POINTER(Grads), vp, vp, sz, vp]
     v = lib.gnca_abi_version()
     if v != ABI_VERSION:
         raise GncaError(f"libgnca.so ABI version {v} != expected {ABI_VERSION}; rebuild it")

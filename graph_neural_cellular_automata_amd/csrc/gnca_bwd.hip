@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_coef(const double* stats, con
 // BB: the MFMA kernel
 // ------------------------------------------------------------------------------------------
 struct BBLayout {
-  int xs, PSTR, al, ALW, sp, kp, w1s, SW1, w2s, SW2, wms, SWM, b1s, bms, percs, wts, scr;
+  int xs, PSTR, al, ALW, sp, kp, w1f, KSP, w1t, S1T, w2t, S2T, wms, SWM, b1s, bms, percs, wts, scr;
   int ST1, ST2, ST3, SCRW, RH, RW, total;
 };
 
@@ -232,20 +232,23 @@ __host__ __device__ inline BBLayout bb_layout(int CP, int HB, int TH, int TW, in
   L.PSTR = r4(L.RH * L.RW);
   L.ALW = L.RW + 2;
   const int CPM = 16 * ((CP + 15) / 16);   // channel rows padded to whole 16-row MFMA tiles
-  L.SW1 = odd4(3 * CP);
-  L.SW2 = odd4(HB);
+  const int MT = HB / 16, MO = (CP + 15) / 16, FT = (3 * CP + 15) / 16;
+  L.KSP = odd4(3 * CP / 4);   // MFMA A-fragments, one 16-byte LDS read per 4 k-steps (as K1)
+  L.S1T = odd4(4 * MT);
+  L.S2T = odd4(4 * MO);
   L.SWM = odd4(CPM);
   L.ST1 = s16(HB);
   L.ST2 = s16(3 * CP);
   L.ST3 = s16(CP);
-  L.SCRW = 16 * (L.ST1 + L.ST2 + 2 * L.ST3);
+  L.SCRW = 16 * (L.ST1 + std::max(L.ST2, 2 * L.ST3));   // T3/T4 reuse T2's rows (after dW1)
   int o = 0;
   L.xs = o; o += CP * L.PSTR;
   L.al = o; o += r4((L.RH + 2) * L.ALW);
   L.sp = o; o += r4(L.RH * L.RW);
   L.kp = o; o += r4(TH * TW);
-  L.w1s = o; o += HB * L.SW1;
-  L.w2s = o; o += CPM * L.SW2;    // zero rows past C: the MFMA tiles read all 16*MO rows
+  L.w1f = o; o += MT * 64 * L.KSP;   // W1 fragments (GEMM1 recompute)
+  L.w1t = o; o += FT * 64 * L.S1T;   // W1^T fragments (dY = W1^T dh)
+  L.w2t = o; o += MT * 64 * L.S2T;   // W2^T fragments (dh = W2^T d_pre)
   L.wms = o; o += CPM * L.SWM;
   L.b1s = o; o += r4(HB);
   L.bms = o; o += CPM;
@@ -290,13 +293,14 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   const int TH = a.TH, TW = a.TW, RY = a.RY, RX = a.RX;
   const BBLayout L = bb_layout(CP, HB, TH, TW, RY, RX, a.k);
   const int RH = L.RH, RW = L.RW, PSTR = L.PSTR, ALW = L.ALW;
-  const int SW1 = L.SW1, SW2 = L.SW2, SWM = L.SWM, ST1 = L.ST1, ST2 = L.ST2, ST3 = L.ST3;
+  const int KSP = L.KSP, S1T = L.S1T, S2T = L.S2T, SWM = L.SWM, ST1 = L.ST1, ST2 = L.ST2, ST3 = L.ST3;
   float* xs = smem + L.xs;
   float* al = smem + L.al;
   float* sp = smem + L.sp;
   float* fp = smem + L.kp;
-  float* w1s = smem + L.w1s;
-  float* w2s = smem + L.w2s;
+  float* w1f = smem + L.w1f;
+  float* w1t = smem + L.w1t;
+  float* w2t = smem + L.w2t;
   float* wms = smem + L.wms;
   float* b1s = smem + L.b1s;
   float* bms = smem + L.bms;
@@ -317,19 +321,29 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
   float* T1 = smem + L.scr + wave * L.SCRW;   // per-wave transpose scratch [16 cells][...]
   float* T2 = T1 + 16 * ST1;
-  float* T3 = T2 + 16 * ST2;
+  float* T3 = T2;                             // d_pre / dm rows, after T2 (y) has been consumed
   float* T4 = T3 + 16 * ST3;
 
   // ---- weights of this hidden slice -> LDS (row-major; strides chosen bank-conflict-free for
   //      both the forward (W1) and the transposed (W1^T, W2^T, W_M^T) fragment reads) ----
-  for (int idx = tid; idx < HB * SW1; idx += kThreads) {
-    const int r = idx / SW1, slot = idx - r * SW1, hid = h0 + r;
+  auto w1at = [&](int hid, int slot) -> float {   // W1[hid][slot], slot = f*CP + c; 0 = padding
     const int f = slot / CP, c = slot - f * CP;
-    w1s[idx] = (hid < Hd && slot < 3 * CP && c < C) ? a.w1[(size_t)hid * 3 * C + f * C + c] : 0.f;
+    return (hid < Hd && slot < 3 * CP && c < C) ? a.w1[(size_t)hid * 3 * C + f * C + c] : 0.f;
+  };
+  for (int idx = tid; idx < MT * 64 * KSP; idx += kThreads) {   // A[hid][slot], k-step s
+    const int s = idx % KSP, ml = idx / KSP, l = ml & 63, m = ml >> 6;
+    w1f[idx] = s < KS ? w1at(h0 + 16 * m + (l & 15), 4 * s + (l >> 4)) : 0.f;
   }
-  for (int idx = tid; idx < 16 * MO * SW2; idx += kThreads) {
-    const int c = idx / SW2, col = idx - c * SW2, hid = h0 + col;
-    w2s[idx] = (c < C && col < HB && hid < Hd) ? a.w2[(size_t)c * Hd + hid] : 0.f;
+  for (int idx = tid; idx < FT * 64 * S1T; idx += kThreads) {   // A[slot][hid], k-step (m, r)
+    const int e = idx % S1T, fl = idx / S1T, l = fl & 63, ft = fl >> 6;
+    const int m = e >> 2, r = e & 3;
+    w1t[idx] = e < 4 * MT ? w1at(h0 + 16 * m + 4 * (l >> 4) + r, 16 * ft + (l & 15)) : 0.f;
+  }
+  for (int idx = tid; idx < MT * 64 * S2T; idx += kThreads) {   // A[hid][c], k-step (mo, s)
+    const int e = idx % S2T, ml = idx / S2T, l = ml & 63, m = ml >> 6;
+    const int mo = e >> 2, s4 = e & 3;
+    const int c = 16 * mo + 4 * (l >> 4) + s4, hid = h0 + 16 * m + (l & 15);
+    w2t[idx] = (e < 4 * MO && c < C && hid < Hd) ? a.w2[(size_t)c * Hd + hid] : 0.f;
   }
   for (int idx = tid; idx < 16 * MO * SWM; idx += kThreads) {
     const int co = idx / SWM, ci = idx - co * SWM;
@@ -381,11 +395,26 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
 
   const int ncell = TH * TW, ngroups = (ncell + 15) >> 4;
   const size_t HW = (size_t)H * W;
+  const int HWi = H * W;
+  // per-lane dY plane offsets of this lane's MFMA output rows (slot = 16ft+4g+r -> f*C+c), or -1
+  int plo[FT][4];
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int slot = 16 * ft + 4 * g + r, f = slot / CP, c = slot - f * CP;
+      plo[ft][r] = (slot < 3 * CP && c < C) ? (f * C + c) * HWi : -1;
+    }
+  const bool cfull = C == CP;   // no padded channels: every output row is live
   for (int tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
     const float* xb = a.x + (size_t)b * C * HW;
+    const float* Ub = a.U + (size_t)b * C * HW;
+    const float* Db = a.dx + (size_t)b * C * HW;
+    float* dYb = a.dY + (size_t)b * 3 * C * HW;
+    float* dGb = a.dG + (size_t)b * C * HW;
     __syncthreads();
     // ---- staging: channel planes over the (RH x RW) region, alpha with one more ring ----
     for (int e = tid; e < CP * RH * RW; e += kThreads) {
@@ -446,8 +475,23 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       const bool valid = n < ncell && i0 + ti < H && j0 + tj < W;
       if (!valid) { ti = 0; tj = 0; }
       const int pidx = (RY + ti) * RW + (RX + tj);
-      const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
+      const int celli = (i0 + ti) * W + (j0 + tj);
       const float* xg = xs + g * PSTR;
+      // issue this group's U / dx loads first: their latency hides under the recompute below
+      const float keep = valid ? fp[n] : 0.f;   // invalid (padding) lanes contribute nothing
+      float ul[MO][4], dl[MO][4];
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 16 * mo + 4 * g + r;
+          ul[mo][r] = 0.f;
+          dl[mo][r] = 0.f;
+          if (keep != 0.f && c < C) {
+            ul[mo][r] = Ub[c * HWi + celli];
+            if (gn) dl[mo][r] = Db[c * HWi + celli];
+          }
+        }
 
       // -- gather (recompute) --
       float gv[CPQ];
@@ -502,10 +546,16 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
 #pragma unroll
       for (int m = 0; m < MT; ++m) hp[m] = *reinterpret_cast<const f4*>(b1s + 16 * m + 4 * g);
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
+      for (int s0 = 0; s0 < KS; s0 += 4) {
+        f4 w4[MT];
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
-          hp[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1s[(16 * m + c16) * SW1 + 4 * s + g], y[s], hp[m], 0, 0, 0);
+        for (int m = 0; m < MT; ++m) w4[m] = *reinterpret_cast<const f4*>(w1f + (m * 64 + lane) * KSP + s0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            if (s0 + u < KS) hp[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[m][u], y[s0 + u], hp[m], 0, 0, 0);
+      }
       // -- message (recompute): m[c = 16mo+4g+r][cell] = W_M G + b_M S --
       f4 mm[MO];
 #pragma unroll
@@ -523,33 +573,28 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       }
       __builtin_amdgcn_sched_barrier(0);
       // -- d_pre = keep * GroupNorm-backward(U) (ncagraph.py:144-153) --
-      const float keep = fp[valid ? n : 0];
       f4 dp[MO];
 #pragma unroll
       for (int mo = 0; mo < MO; ++mo)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int c = 16 * mo + 4 * g + r;
-          float v = 0.f;
-          if (valid && c < C && keep != 0.f) {
-            const size_t p = ((size_t)b * C + c) * HW + cell;
-            const float u = a.U[p];
-            v = gn ? rs * (u - mu_u - (a.dx[p] - mu) * rs * mu_ux) : u;
-          }
-          dp[mo][r] = v;
+          const float u = ul[mo][r];
+          const bool live = keep != 0.f && 16 * mo + 4 * g + r < C;
+          dp[mo][r] = live ? (gn ? rs * (u - mu_u - (dl[mo][r] - mu) * rs * mu_ux) : u) : 0.f;
         }
       // -- dh = relu'(hpre) * W2^T d_pre --
       f4 dh[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) dh[m] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int m = 0; m < MT; ++m) {
+        dh[m] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int mo = 0; mo < MO; ++mo)
+        for (int mo = 0; mo < MO; ++mo) {
+          const f4 wv = *reinterpret_cast<const f4*>(w2t + (m * 64 + lane) * S2T + 4 * mo);
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int m = 0; m < MT; ++m)
-            dh[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2s[(16 * mo + 4 * g + s) * SW2 + 16 * m + c16],
-                                                         dp[mo][s], dh[m], 0, 0, 0);
+          for (int s4 = 0; s4 < 4; ++s4)
+            dh[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[s4], dp[mo][s4], dh[m], 0, 0, 0);
+        }
+      }
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -558,25 +603,41 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
           hp[m][r] = hp[m][r] > 0.f ? hp[m][r] : (hp[m][r] != hp[m][r] ? hp[m][r] : 0.f);  // relu
         }
       __builtin_amdgcn_sched_barrier(0);
-      // -- dY = W1^T dh -> HBM (slot = f*CP + c -> plane f*C + c) --
+      // -- dY = W1^T dh -> HBM (slot = f*CP + c -> plane f*C + c); FT independent chains --
+      {
+        f4 ay[FT];
 #pragma unroll
-      for (int ft = 0; ft < FT; ++ft) {
-        f4 ay = f4{0.f, 0.f, 0.f, 0.f};
+        for (int ft = 0; ft < FT; ++ft) ay[ft] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
+        for (int m = 0; m < MT; ++m) {
+          f4 wv[FT];
+#pragma unroll
+          for (int ft = 0; ft < FT; ++ft) wv[ft] = *reinterpret_cast<const f4*>(w1t + (ft * 64 + lane) * S1T + 4 * m);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            ay = __builtin_amdgcn_mfma_f32_16x16x4f32(w1s[(16 * m + 4 * g + r) * SW1 + 16 * ft + c16],
-                                                      dh[m][r], ay, 0, 0, 0);
-        if (valid) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int slot = 16 * ft + 4 * g + r;
-            if (slot >= 3 * CP) continue;
-            const int f = slot / CP, c = slot - f * CP;
-            if (c >= C) continue;
-            float* p = a.dY + ((size_t)b * 3 * C + f * C + c) * HW + cell;
-            *p = first ? ay[r] : *p + ay[r];
+            for (int ft = 0; ft < FT; ++ft)
+              ay[ft] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[ft][r], dh[m][r], ay[ft], 0, 0, 0);
+        }
+        if (valid) {
+          float* q = dYb + celli;
+          if (first && cfull && 16 * FT == 3 * CP) {
+#pragma unroll
+            for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) q[plo[ft][r]] = ay[ft][r];
+          } else if (first) {
+#pragma unroll
+            for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (plo[ft][r] >= 0) q[plo[ft][r]] = ay[ft][r];
+          } else {
+#pragma unroll
+            for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (plo[ft][r] >= 0) q[plo[ft][r]] += ay[ft][r];
           }
         }
       }
@@ -604,17 +665,22 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
             for (int s = 0; s < 4; ++s)
               ag = __builtin_amdgcn_mfma_f32_16x16x4f32(wms[(16 * mo + 4 * g + s) * SWM + 16 * mi + c16],
                                                         dm[mo][s], ag, 0, 0, 0);
-          if (valid)
+          if (valid) {
+            float* q = dGb + (16 * mi + 4 * g) * HWi + celli;
+            if (cfull && (CP & 15) == 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int ci = 16 * mi + 4 * g + r;
-              if (ci < C) a.dG[((size_t)b * C + ci) * HW + cell] = ag[r];
+              for (int r = 0; r < 4; ++r) q[r * HWi] = ag[r];
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (16 * mi + 4 * g + r < C) q[r * HWi] = ag[r];
             }
+          }
         }
         if (a.dmb) {
           dmb += __shfl_xor(dmb, 16);
           dmb += __shfl_xor(dmb, 32);
-          if (valid && g == 0) a.dmb[(size_t)b * HW + cell] = dmb;
+          if (valid && g == 0) a.dmb[(size_t)b * HW + celli] = dmb;
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -739,80 +805,126 @@ struct BCArgs {
   int8_t offs[2 * GNCA_MAX_OFFSETS];
 };
 
+constexpr int kBCStage = 16;   // max staged elements per thread per channel
+
+__host__ __device__ inline int bc_stage(int TH, int TW, int RY, int RX, bool msg) {
+  return 3 * (TH + 2) * (TW + 2) + (msg ? (TH + 2 * RY) * (TW + 2 * RX) : 0);
+}
+
+// One workgroup per (sample, tile); channels are pipelined through a double-buffered LDS
+// stage (the next channel's dY planes and dG halo are loaded into registers while this channel
+// is computed), one barrier per channel.
 __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int b = blockIdx.x / a.tps, tin = blockIdx.x - b * a.tps;
   const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
-  const int TH = a.TH, TW = a.TW, RY = a.RY, RX = a.RX, H = a.H, W = a.W, C = a.C, k = a.k;
+  const int RY = a.RY, RX = a.RX, H = a.H, W = a.W, C = a.C, k = a.k;
+  const int TH = a.TH, TW = a.TW, PW = TW + 2, PA = (TH + 2) * PW;
   const int i0 = ty * TH, j0 = tx * TW;
   const size_t HW = (size_t)H * W;
   const bool zp = (a.flags & GNCA_ZERO_PAD_SHIFT) != 0;
   const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
   const bool msg = (a.flags & kMsg) != 0;
-  const int PW = TW + 2, PA = (TH + 2) * PW;          // ring-1 planes
-  const int GW = TW + 2 * RX, GA = (TH + 2 * RY) * GW;  // gather-halo plane
-  float* dy3 = smem;                  // 3 x PA
-  float* dgp = dy3 + 3 * PA;          // GA
-  float* as_ = dgp + GA;              // TH*TW sender mask of the tile cells
-  float* wts = as_ + TH * TW;         // k
-  float* alr = wts + (k > 0 ? k : 1); // PA alpha ring (-inf outside)
+  const int GW = TW + 2 * RX;
+  const int SE = bc_stage(TH, TW, RY, RX, msg);       // staged floats per channel
+  float* buf0 = smem;
+  float* buf1 = smem + SE;
+  float* as_ = buf1 + SE;                              // [TH*TW] sender mask of the tile cells
+  float* wts = as_ + TH * TW;                          // [k]
+  float* pws = wts + (k > 0 ? k : 1);                  // [C*27] perception weights
   const float* xb = a.x + (size_t)b * C * HW;
+  for (int e = tid; e < C * 27; e += kThreads) pws[e] = a.perc[e];
   if (msg) {
-    for (int e = tid; e < PA; e += kThreads) {
-      const int ii = i0 - 1 + e / PW, jj = j0 - 1 + e % PW;
-      alr[e] = (ii >= 0 && ii < H && jj >= 0 && jj < W) ? xb[3 * HW + (size_t)ii * W + jj] : -INFINITY;
-    }
     for (int o = tid; o < k; o += kThreads) wts[o] = a.offw ? a.offw[(size_t)b * k + o] : a.uniform_w;
-    __syncthreads();
     for (int n = tid; n < TH * TW; n += kThreads) {
-      const int ti = n / TW, tj = n % TW;
+      const int i = i0 + n / TW, j = j0 + n % TW;
       float mx = -INFINITY;
-      for (int u = 0; u < 3; ++u)
-        for (int v = 0; v < 3; ++v) mx = fmaxf(mx, alr[(ti + u) * PW + tj + v]);
+      if (i < H && j < W)
+        for (int u = max(0, i - 1); u <= min(H - 1, i + 1); ++u)
+          for (int v = max(0, j - 1); v <= min(W - 1, j + 1); ++v) mx = fmaxf(mx, xb[3 * HW + (size_t)u * W + v]);
       as_[n] = a2a ? (mx > a.graph_alpha_thr ? 1.f : 0.f) : 1.f;
     }
   }
-  for (int c = 0; c < C; ++c) {
-    __syncthreads();
-    for (int e = tid; e < 3 * PA; e += kThreads) {
+  // per-thread staging plan: element e = tid + 256*i of [3 dY planes | dG halo]; source offset
+  // within the channel plane (or -1 = zero), and the plane group (0..2 dY, 3 dG)
+  int soff[kBCStage];
+  int sgrp[kBCStage];
+#pragma unroll
+  for (int i = 0; i < kBCStage; ++i) {
+    const int e = tid + kThreads * i;
+    soff[i] = -1;
+    sgrp[i] = -1;
+    if (e >= SE) continue;
+    if (e < 3 * PA) {
       const int f = e / PA, r = e - f * PA;
       const int ii = i0 - 1 + r / PW, jj = j0 - 1 + r % PW;
-      dy3[e] = (ii >= 0 && ii < H && jj >= 0 && jj < W)
-                   ? a.dY[((size_t)b * 3 * C + f * C + c) * HW + (size_t)ii * W + jj] : 0.f;
+      sgrp[i] = f;
+      if (ii >= 0 && ii < H && jj >= 0 && jj < W) soff[i] = ii * W + jj;
+    } else {
+      const int r = e - 3 * PA;
+      int ii = i0 - RY + r / GW, jj = j0 - RX + r % GW;
+      bool ok = true;
+      if (zp) ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
+      else { ii = wrapi(ii, H); jj = wrapi(jj, W); }
+      sgrp[i] = 3;
+      if (ok) soff[i] = ii * W + jj;
     }
-    if (msg)
-      for (int e = tid; e < GA; e += kThreads) {
-        int ii = i0 - RY + e / GW, jj = j0 - RX + e % GW;
-        bool ok = true;
-        if (zp) ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
-        else { ii = wrapi(ii, H); jj = wrapi(jj, W); }
-        dgp[e] = ok ? a.dG[((size_t)b * C + c) * HW + (size_t)ii * W + jj] : 0.f;
+  }
+  float stg[kBCStage];
+  auto load = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < kBCStage; ++i) {
+      float v = 0.f;
+      if (soff[i] >= 0) {
+        const float* base = sgrp[i] < 3 ? a.dY + ((size_t)b * 3 * C + sgrp[i] * C + c) * HW
+                                        : a.dG + ((size_t)b * C + c) * HW;
+        v = base[soff[i]];
       }
-    __syncthreads();
-    const float* pw = a.perc + (size_t)3 * c * 9;
+      stg[i] = v;
+    }
+  };
+  auto store = [&](float* dst) {
+#pragma unroll
+    for (int i = 0; i < kBCStage; ++i)
+      if (tid + kThreads * i < SE) dst[tid + kThreads * i] = stg[i];
+  };
+  load(0);
+  store(buf0);
+  __syncthreads();
+  for (int c = 0; c < C; ++c) {
+    float* cur = (c & 1) ? buf1 : buf0;
+    float* nxt = (c & 1) ? buf0 : buf1;
+    if (c + 1 < C) load(c + 1);
+    const float* pw = pws + c * 27;
     for (int n = tid; n < TH * TW; n += kThreads) {
       const int ti = n / TW, tj = n % TW;
       const int i = i0 + ti, j = j0 + tj;
       if (i >= H || j >= W) continue;
       // y(p) += w[u][v] x(p + (u-1, v-1))  =>  gx(q) += w[u][v] dY(q - (u-1, v-1))
       float acc = 0.f;
+#pragma unroll
       for (int f = 0; f < 3; ++f)
+#pragma unroll
         for (int u = 0; u < 3; ++u)
+#pragma unroll
           for (int v = 0; v < 3; ++v)
-            acc = fmaf(pw[f * 9 + u * 3 + v], dy3[f * PA + (ti + 2 - u) * PW + (tj + 2 - v)], acc);
+            acc = fmaf(pw[f * 9 + u * 3 + v], cur[f * PA + (ti + 2 - u) * PW + (tj + 2 - v)], acc);
       if (msg) {
         // msg(p) = sum_o w_o A(p-o) M(p-o)  =>  gM(q) = A(q) sum_o w_o dm(q+o)  (roll / row shift)
+        const float* g0 = cur + 3 * PA + (ti + RY) * GW + (tj + RX);
         float sg = 0.f;
         for (int o = 0; o < k; ++o) {
           const int dy = a.offs[2 * o], dx = zp ? 0 : a.offs[2 * o + 1];
-          sg = fmaf(wts[o], dgp[(ti + RY + dy) * GW + (tj + RX + dx)], sg);
+          sg = fmaf(wts[o], g0[dy * GW + dx], sg);
         }
         acc = fmaf(as_[n], sg, acc);
       }
       float* p = a.gx + ((size_t)b * C + c) * HW + (size_t)i * W + j;
       *p += acc;
     }
+    if (c + 1 < C) store(nxt);
+    __syncthreads();
   }
 }
 
@@ -1022,21 +1134,56 @@ __global__ __launch_bounds__(kThreads) void gnca_b_rowcorr(float* gx, const floa
   }
 }
 
-// R: out[j] = sum_r part[r*stride + col0 + j*step], r in fixed order (deterministic)
-__global__ __launch_bounds__(kThreads) void gnca_b_reduce(const void* part, int f64, long rows, long stride,
-                                                          long col0, int ncols, int step, float* out) {
-  const int j = blockIdx.x * kThreads + threadIdx.x;
-  if (j >= ncols) return;
-  double s = 0.0;
-  const long col = col0 + (long)j * step;
-  if (f64) {
-    const double* p = reinterpret_cast<const double*>(part);
-    for (long r = 0; r < rows; ++r) s += p[r * stride + col];
-  } else {
-    const float* p = reinterpret_cast<const float*>(part);
-    for (long r = 0; r < rows; ++r) s += (double)p[r * stride + col];
+// R: fixed-order sums of partial rows into the gradient outputs (deterministic).
+// The output columns of up to 8 segments are numbered consecutively; segment s maps its local
+// column j to part column col0[s] + j*step[s] and writes out[s][j] (skipped if out[s] is null).
+// A 256-thread block owns 16 columns: 16 row groups sum rows r = g, g+16, ... with 4 independent
+// accumulators each, then the 16 group sums are added in order.
+struct RedArgs {
+  const void* part;
+  int f64;
+  long rows, stride;
+  int nseg, ncols;
+  int end[8];       // exclusive end of segment s in the concatenated column space
+  long col0[8];
+  int step[8];
+  float* out[8];
+};
+
+__global__ __launch_bounds__(kThreads) void gnca_b_reduce(const RedArgs a) {
+  __shared__ double acc[16][17];
+  const int cj = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + cj;
+  int s = 0;
+  while (s < a.nseg - 1 && col >= a.end[s]) ++s;
+  const int begin = s == 0 ? 0 : a.end[s - 1];
+  const long src = a.col0[s] + (long)(col - begin) * a.step[s];
+  double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+  if (col < a.ncols) {
+    long r = rg;
+    if (a.f64) {
+      const double* p = reinterpret_cast<const double*>(a.part) + src;
+      for (; r + 48 < a.rows; r += 64) {
+        t0 += p[r * a.stride]; t1 += p[(r + 16) * a.stride];
+        t2 += p[(r + 32) * a.stride]; t3 += p[(r + 48) * a.stride];
+      }
+      for (; r < a.rows; r += 16) t0 += p[r * a.stride];
+    } else {
+      const float* p = reinterpret_cast<const float*>(a.part) + src;
+      for (; r + 48 < a.rows; r += 64) {
+        t0 += (double)p[r * a.stride]; t1 += (double)p[(r + 16) * a.stride];
+        t2 += (double)p[(r + 32) * a.stride]; t3 += (double)p[(r + 48) * a.stride];
+      }
+      for (; r < a.rows; r += 16) t0 += (double)p[r * a.stride];
+    }
   }
-  out[j] = (float)s;
+  acc[rg][cj] = (t0 + t1) + (t2 + t3);
+  __syncthreads();
+  if (rg == 0 && col < a.ncols && a.out[s]) {
+    double v = 0.0;
+    for (int g = 0; g < 16; ++g) v += acc[g][cj];
+    a.out[s][col - begin] = (float)v;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1050,7 +1197,8 @@ struct BBVariant {
 static const BBVariant kBB[] = {
     GNCA_BV(16, 128), GNCA_BV(4, 32),  GNCA_BV(8, 32),  GNCA_BV(16, 32), GNCA_BV(4, 64),
     GNCA_BV(8, 64),   GNCA_BV(12, 64), GNCA_BV(16, 64), GNCA_BV(20, 64), GNCA_BV(24, 64),
-    GNCA_BV(28, 64),  GNCA_BV(32, 64),
+    GNCA_BV(28, 64),  GNCA_BV(32, 64), GNCA_BV(12, 32), GNCA_BV(20, 32), GNCA_BV(24, 32),
+    GNCA_BV(28, 32),  GNCA_BV(32, 32),
 };
 #undef GNCA_BV
 
@@ -1094,19 +1242,6 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   P->msg = P->graph && P->F.k > 0 && d->message_gain != 0.f;
   P->zp = (d->flags & GNCA_ZERO_PAD_SHIFT) != 0;
   P->gn = (d->flags & GNCA_USE_GROUPNORM) != 0;
-  // hidden slice width: the largest compiled HB <= 128 for this CP that is not much wider than Hd
-  P->bb = nullptr;
-  for (const BBVariant& v : kBB) {
-    if (v.CP != P->CP) continue;
-    if (!P->bb) { P->bb = &v; continue; }
-    const int cur = P->bb->HB;
-    const bool cur_fits = cur >= Hd, v_fits = v.HB >= Hd;
-    if (v_fits && (!cur_fits || v.HB < cur)) P->bb = &v;
-    else if (!v_fits && !cur_fits && v.HB > cur) P->bb = &v;
-  }
-  if (!P->bb) return false;
-  P->HB = P->bb->HB;
-  P->nslices = (Hd + P->HB - 1) / P->HB;
   int ry = 1, rx = 1;
   if (P->msg)
     for (int o = 0; o < P->F.k; ++o) {
@@ -1115,22 +1250,34 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
     }
   P->RY = ry;
   P->RX = rx;
-  // BB tile: fewest padded cells + staged halo within 160 KB LDS
+  // hidden slice (variant) and BB tile: fewest slices first (each slice recomputes the
+  // perception, gather and message), then fewest padded hidden units, then the cheapest tile
+  // (padded cells + staged halo) within 160 KB of LDS
   static const int ths[] = {4, 8, 16};
   static const int tws[] = {8, 16, 24, 32};
   double best = 1e300;
-  P->TH = 0;
-  for (int th : ths)
-    for (int tw : tws) {
-      if ((th * tw) % 64) continue;
-      const BBLayout L = bb_layout(P->CP, P->HB, th, tw, ry, rx, P->F.k);
-      const size_t bytes = (size_t)L.total * 4;
-      if (bytes > 160 * 1024) continue;
-      const long tx = (W + tw - 1) / tw, ty = (H + th - 1) / th;
-      const double cost = (double)tx * ty * th * tw + 0.01 * tx * ty * L.RH * L.RW * P->CP + 30.0 * tx * ty;
-      if (cost < best) { best = cost; P->TH = th; P->TW = tw; P->ldsB = bytes; }
-    }
-  if (!P->TH) return false;
+  P->bb = nullptr;
+  for (const BBVariant& v : kBB) {
+    if (v.CP != P->CP) continue;
+    const int ns = (Hd + v.HB - 1) / v.HB;
+    const int padh = ns * v.HB - Hd;
+    for (int th : ths)
+      for (int tw : tws) {
+        if ((th * tw) % 64) continue;
+        const BBLayout L = bb_layout(P->CP, v.HB, th, tw, ry, rx, P->F.k);
+        const size_t bytes = (size_t)L.total * 4;
+        if (bytes > 160 * 1024) continue;
+        const long tx = (W + tw - 1) / tw, ty = (H + th - 1) / th;
+        const double tcost = (double)tx * ty * th * tw + 0.01 * tx * ty * L.RH * L.RW * P->CP + 30.0 * tx * ty;
+        const double cost = 1e12 * ns + 1e9 * padh + tcost;
+        if (cost < best) {
+          best = cost; P->bb = &v; P->TH = th; P->TW = tw; P->ldsB = bytes;
+        }
+      }
+  }
+  if (!P->bb) return false;
+  P->HB = P->bb->HB;
+  P->nslices = (Hd + P->HB - 1) / P->HB;
   P->tiles_x = (W + P->TW - 1) / P->TW;
   P->tps = P->tiles_x * ((H + P->TH - 1) / P->TH);
   P->total_tiles = P->tps * d->B;
@@ -1147,15 +1294,26 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
     P->ldsA = (size_t)(2 * P->band + 2) * W * 4;
     if (P->ldsA > 64 * 1024) return false;
   }
-  // BC tiles
-  P->TH3 = 16;
-  P->TW3 = 16;
-  P->tiles_x3 = (W + P->TW3 - 1) / P->TW3;
-  P->tps3 = P->tiles_x3 * ((H + P->TH3 - 1) / P->TH3);
+  // BC tiles: fewest padded cells + staged halo, within the per-thread staging registers
   {
-    const int PA = (P->TH3 + 2) * (P->TW3 + 2);
-    const int GA = (P->TH3 + 2 * ry) * (P->TW3 + 2 * (P->zp ? 0 : rx));
-    P->ldsC = (size_t)(3 * PA + GA + P->TH3 * P->TW3 + std::max(P->F.k, 1) + PA) * 4;
+    static const int bth[] = {8, 12, 16, 24, 32};
+    static const int btw[] = {16, 24, 32, 48, 64};
+    const int rxc = P->zp ? 0 : rx;
+    double bestc = 1e300;
+    P->TH3 = 0;
+    for (int th : bth)
+      for (int tw : btw) {
+        const int se = bc_stage(th, tw, ry, rxc, P->msg);
+        if (se > kBCStage * kThreads || th * tw > 4 * kThreads) continue;
+        const long tx = (W + tw - 1) / tw, ty = (H + th - 1) / th;
+        const double cost = (double)tx * ty * (th * tw + 0.25 * se);
+        if (cost < bestc) { bestc = cost; P->TH3 = th; P->TW3 = tw; }
+      }
+    if (!P->TH3) return false;
+    P->tiles_x3 = (W + P->TW3 - 1) / P->TW3;
+    P->tps3 = P->tiles_x3 * ((H + P->TH3 - 1) / P->TH3);
+    P->ldsC = (size_t)(2 * bc_stage(P->TH3, P->TW3, ry, rxc, P->msg) + P->TH3 * P->TW3 +
+                       std::max(P->F.k, 1) + 27 * C) * 4;
   }
   P->rows_per = std::max(1, (int)((4096 + W - 1) / W));
   P->nrb = (H + P->rows_per - 1) / P->rows_per;
@@ -1198,13 +1356,27 @@ static int bwd_check() {
   return GNCA_OK;
 }
 
-static int reduce_into(const void* part, bool f64, long rows, long stride, long col0, int ncols,
-                       int step, float* out, hipStream_t st) {
-  if (!out || ncols <= 0) return GNCA_OK;
-  hipLaunchKernelGGL(gnca_b_reduce, dim3((ncols + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                     part, f64 ? 1 : 0, rows, stride, col0, ncols, step, out);
-  return bwd_check();
-}
+struct Reducer {
+  RedArgs a;
+  Reducer(const void* part, bool f64, long rows, long stride) {
+    memset(&a, 0, sizeof(a));
+    a.part = part; a.f64 = f64 ? 1 : 0; a.rows = rows; a.stride = stride;
+  }
+  void add(long col0, int ncols, int step, float* out) {
+    if (ncols <= 0) return;
+    a.col0[a.nseg] = col0;
+    a.step[a.nseg] = step;
+    a.out[a.nseg] = out;
+    a.ncols += ncols;
+    a.end[a.nseg] = a.ncols;
+    ++a.nseg;
+  }
+  int launch(hipStream_t st) {
+    if (a.nseg == 0 || a.ncols == 0) return GNCA_OK;
+    hipLaunchKernelGGL(gnca_b_reduce, dim3((a.ncols + 15) / 16), dim3(kThreads), 0, st, a);
+    return bwd_check();
+  }
+};
 
 static int zero_grad(float* p, size_t n, hipStream_t st) {
   if (!p || n == 0) return GNCA_OK;
@@ -1226,7 +1398,7 @@ size_t gnca_bwd_workspace_bytes(const gnca_step_desc* desc) {
 
 int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
                       const void* fire, const float* gy, float* gx, const gnca_grads* grads,
-                      void* ws, size_t ws_bytes, void* stream) {
+                      const void* saved, void* ws, size_t ws_bytes, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (!desc || !w || !x || !gy || !gx || !grads) return GNCA_ERR_INVALID;
   if (gx == x || gx == gy) return GNCA_ERR_INVALID;
@@ -1244,12 +1416,13 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
   int rc;
   // F: recompute the forward's dx / GroupNorm partials / offset weights (gx is a dummy x_out:
   // phase K2, the only writer of x_out, is not run)
-  if ((rc = gnca_step_phases_f32(&d, w, x, gx, fire, nullptr, wsb + P.off_fwd, P.F.ws_bytes, stream,
-                                 GNCA_PHASE_K0 | GNCA_PHASE_K1)) != GNCA_OK)
+  const char* fw = saved ? reinterpret_cast<const char*>(saved) : wsb + P.off_fwd;
+  if (!saved && (rc = gnca_step_phases_f32(&d, w, x, gx, fire, nullptr, wsb + P.off_fwd, P.F.ws_bytes,
+                                           stream, GNCA_PHASE_K0 | GNCA_PHASE_K1)) != GNCA_OK)
     return rc;
-  const float* dx = reinterpret_cast<const float*>(wsb + P.off_fwd + P.F.off_dx);
-  const double* stats = reinterpret_cast<const double*>(wsb + P.off_fwd + P.F.off_stats);
-  const float* offw = (P.msg && P.zp) ? reinterpret_cast<const float*>(wsb + P.off_fwd + P.F.off_offw) : nullptr;
+  const float* dx = reinterpret_cast<const float*>(fw + P.F.off_dx);
+  const double* stats = reinterpret_cast<const double*>(fw + P.F.off_stats);
+  const float* offw = (P.msg && P.zp) ? reinterpret_cast<const float*>(fw + P.F.off_offw) : nullptr;
   float* U = reinterpret_cast<float*>(wsb + P.off_U);
   float* dY = reinterpret_cast<float*>(wsb + P.off_dY);
   float* dG = reinterpret_cast<float*>(wsb + P.off_dG);
@@ -1317,20 +1490,24 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     hipLaunchKernelGGL(gnca_b_adjoint, dim3(B * P.tps3), dim3(kThreads), P.ldsC, st, a);
     if ((rc = bwd_check()) != GNCA_OK) return rc;
   }
-  const long rowsB = (long)P.gridB * NW;
-  if ((rc = reduce_into(pb, false, rowsB, P.npart, P.o_w1, Hd * 3 * C, 1, grads->w1, st)) ||
-      (rc = reduce_into(pb, false, rowsB, P.npart, P.o_b1, Hd, 1, grads->b1, st)) ||
-      (rc = reduce_into(pb, false, rowsB, P.npart, P.o_w2, C * Hd, 1, grads->w2, st)))
-    return rc;
+  {
+    Reducer r(pb, false, (long)P.gridB * NW, P.npart);
+    r.add(P.o_w1, Hd * 3 * C, 1, grads->w1);
+    r.add(P.o_b1, Hd, 1, grads->b1);
+    r.add(P.o_w2, C * Hd, 1, grads->w2);
+    if (P.graph) {
+      r.add(P.o_wm, C * C, 1, grads->wm);
+      r.add(P.o_bm, C, 1, grads->bm);
+    }
+    if ((rc = r.launch(st)) != GNCA_OK) return rc;
+  }
   if (P.gn) {
-    if ((rc = reduce_into(pa, true, (long)B * P.nbands, 2 + 2 * C, 2, C, 2, grads->gn_weight, st)) ||
-        (rc = reduce_into(pa, true, (long)B * P.nbands, 2 + 2 * C, 3, C, 2, grads->gn_bias, st)))
-      return rc;
+    Reducer r(pa, true, (long)B * P.nbands, 2 + 2 * C);
+    r.add(2, C, 2, grads->gn_weight);
+    r.add(3, C, 2, grads->gn_bias);
+    if ((rc = r.launch(st)) != GNCA_OK) return rc;
   }
   if (!P.graph) return GNCA_OK;
-  if ((rc = reduce_into(pb, false, rowsB, P.npart, P.o_wm, C * C, 1, grads->wm, st)) ||
-      (rc = reduce_into(pb, false, rowsB, P.npart, P.o_bm, C, 1, grads->bm, st)))
-    return rc;
   const int dmod = std::max(d.d_model, 1);
   if (!(P.msg && P.zp)) {  // torus (or no message): the offset weights are constants
     if ((rc = zero_grad(grads->wq, (size_t)dmod * C, st)) || (rc = zero_grad(grads->bq, dmod, st)) ||
@@ -1370,13 +1547,16 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
                        B, C, H, W);
     if ((rc = bwd_check()) != GNCA_OK) return rc;
   }
-  const int dq = d.d_model;
-  if ((rc = reduce_into(pq, true, B, P.nq, 0, dq * C, 1, grads->wq, st)) ||
-      (rc = reduce_into(pq, true, B, P.nq, dq * C, dq, 1, grads->bq, st)) ||
-      (rc = reduce_into(pq, true, B, P.nq, dq * C + dq, dq * C, 1, grads->wk, st)) ||
-      (rc = reduce_into(pq, true, B, P.nq, 2 * dq * C + dq, dq, 1, grads->bk, st)) ||
-      (rc = reduce_into(pq, true, B, P.nq, 2 * dq * C + 2 * dq, 1, 1, grads->scaling, st)))
-    return rc;
+  {
+    const int dq = d.d_model;
+    Reducer r(pq, true, B, P.nq);
+    r.add(0, dq * C, 1, grads->wq);
+    r.add(dq * C, dq, 1, grads->bq);
+    r.add(dq * C + dq, dq * C, 1, grads->wk);
+    r.add(2 * dq * C + dq, dq, 1, grads->bk);
+    r.add(2 * dq * C + 2 * dq, 1, 1, grads->scaling);
+    if ((rc = r.launch(st)) != GNCA_OK) return rc;
+  }
   return GNCA_OK;
 }
 

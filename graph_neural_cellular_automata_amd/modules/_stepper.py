@@ -11,20 +11,24 @@ from .. import step as S
 class _StepFn(torch.autograd.Function):
     """The HIP step as an autograd node (BPTT through the trainers' rollouts).
 
-    Forward: ``gnca_step_f32``.  Backward: ``gnca_step_bwd_f32``, which recomputes the step's
-    intermediates from the saved input state, so a rollout keeps only its states alive (as the
-    reference's autograd graph would, minus the per-op activations).  Gradients follow the
+    Forward: ``gnca_step_f32`` into a workspace that the node keeps (the step's update field and
+    GroupNorm partials, ~one state of memory).  Backward: ``gnca_step_bwd_f32`` on that saved
+    workspace; everything else (perception, hidden layer, message) is recomputed from the input
+    state, so a rollout keeps two state-sized tensors per step alive, far less than the
+    reference's per-op activations.  Gradients follow the
     reference's graph of tensors: masks are constants, the perception weight is frozen,
     ``gate_mlp`` is never used (None), and the graph parameters get None when no offsets were
     drawn (``graph_augmentation.py:141-147`` returns zeros without touching them)."""
 
     @staticmethod
     def forward(ctx, x, desc, weights, keep, fire, want_attn, names, *params):
-        out, attn = S.step(desc, weights, x, fire=fire, want_attention=want_attn)
+        ws = S.workspace(desc, x.device)   # kept: the backward reuses its update field
+        out, attn = S.step(desc, weights, x, fire=fire, want_attention=want_attn, ws=ws)
         if attn is not None:
             ctx.mark_non_differentiable(attn)
         ctx.save_for_backward(x)
         ctx.desc, ctx.weights, ctx.keep, ctx.fire, ctx.names = desc, weights, keep, fire, names
+        ctx.ws = ws
         ctx.params = params
         return out, attn
 
@@ -41,7 +45,9 @@ class _StepFn(torch.autograd.Function):
             if no_graph_use and name.startswith("graph."):
                 continue
             want[name] = p
-        gx, grads = S.step_backward(desc, ctx.weights, x, gout.contiguous(), fire=ctx.fire, want=want)
+        gx, grads = S.step_backward(desc, ctx.weights, x, gout.contiguous(), fire=ctx.fire, want=want,
+                                    saved=ctx.ws)
+        ctx.ws = None
         pgrads = [grads.get(n) for n in ctx.names]
         return (gx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, *pgrads)
 

@@ -90,13 +90,15 @@ def stream_ptr(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-def step(desc, weights, x, fire=None, want_attention=False):
-    """One step: returns (x_out, attn_or_None)."""
+def step(desc, weights, x, fire=None, want_attention=False, ws=None):
+    """One step: returns (x_out, attn_or_None).  ``ws``: an optional caller-owned workspace
+    (``workspace(desc)``); after the call it holds what ``step_backward(saved=ws)`` reuses."""
     lib = L.load()
     x_out = torch.empty_like(x)
     attn = torch.empty(desc.B, desc.H, desc.W, dtype=torch.float32, device=x.device) \
         if want_attention else None
-    ws = workspace(desc, x.device)
+    if ws is None:
+        ws = workspace(desc, x.device)
     rc = lib.gnca_step_f32(ctypes.byref(desc), ctypes.byref(weights), x.data_ptr(),
                            x_out.data_ptr(), _ptr(fire), _ptr(attn), ws.data_ptr(), ws.numel(),
                            stream_ptr(x.device))
@@ -156,11 +158,13 @@ GRAD_FIELDS = {
 }
 
 
-def step_backward(desc, weights, x, gy, fire=None, want: dict | None = None):
+def step_backward(desc, weights, x, gy, fire=None, want: dict | None = None, saved=None):
     """Vector-Jacobian product of one step (gnca_step_bwd_f32).
 
     ``want`` maps state_dict names (GRAD_FIELDS keys) to the parameter tensors whose gradients
-    are wanted; returns ``(gx, {name: grad})`` with grads shaped like the parameters."""
+    are wanted; returns ``(gx, {name: grad})`` with grads shaped like the parameters.
+    ``saved``: the workspace of the forward ``step(..., ws=saved)`` call on the same inputs
+    (skips recomputing the forward's update field)."""
     lib = L.load()
     gy = _dev_f32(gy, "grad_output")
     gx = torch.empty_like(x)
@@ -177,7 +181,7 @@ def step_backward(desc, weights, x, gy, fire=None, want: dict | None = None):
             f"W={desc.W} hidden={desc.hidden}")
     ws = torch.empty(n, dtype=torch.uint8, device=x.device)
     rc = lib.gnca_step_bwd_f32(ctypes.byref(desc), ctypes.byref(weights), x.data_ptr(), _ptr(fire),
-                               gy.data_ptr(), gx.data_ptr(), ctypes.byref(g), ws.data_ptr(),
-                               ws.numel(), stream_ptr(x.device))
+                               gy.data_ptr(), gx.data_ptr(), ctypes.byref(g), _ptr(saved),
+                               ws.data_ptr(), ws.numel(), stream_ptr(x.device))
     L.check(rc, "gnca_step_bwd_f32")
     return gx, out

@@ -182,14 +182,16 @@ size_t gnca_bwd_workspace_bytes(const gnca_step_desc* desc);
 /*
  * Vector-Jacobian product of one step: given the step input x (and the same desc, weights and
  * fire input as the forward call) and gy = dL/d x_out, write gx = dL/dx and the parameter
- * gradients.  The step's forward intermediates are recomputed (nothing is saved by the forward).
- * The alive / fire masks are constants, the perception weight is frozen (no gradient), as in the
- * reference's autograd graph.  In torus mode the offset weights are exactly uniform, so the
- * query/key/scaling gradients are exactly zero.  gx must not alias x or gy.
+ * gradients.  The alive / fire masks are constants, the perception weight is frozen (no
+ * gradient), as in the reference's autograd graph.  In torus mode the offset weights are exactly
+ * uniform, so the query/key/scaling gradients are exactly zero.  gx must not alias x or gy.
+ *   saved: the workspace of the gnca_step_f32 call that produced x_out (same desc, weights, x
+ *          and fire), kept unmodified since: its update field and GroupNorm partials are reused.
+ *          NULL: the backward recomputes them (one more forward pass).
  */
 int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
                       const void* fire, const float* gy, float* gx, const gnca_grads* grads,
-                      void* ws, size_t ws_bytes, void* stream);
+                      const void* saved, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

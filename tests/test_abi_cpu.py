@@ -121,5 +121,5 @@ def test_bwd_rejects_bad_args_without_touching_gpu(lib):
     w = L.Weights()
     g = L.Grads()
     rc = lib.gnca_step_bwd_f32(ctypes.byref(d), ctypes.byref(w), None, None, None, None, ctypes.byref(g),
-                               None, 0, None)
+                               None, None, 0, None)
     assert rc == -1

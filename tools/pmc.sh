@@ -5,16 +5,19 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-ARGS="python3 bench.py --steps 4 --warmup 1 --no-cpu ${BENCH_ARGS:-}"
+ARGS="${PMC_CMD:-python3 bench.py --steps 4 --warmup 1 --no-cpu ${BENCH_ARGS:-}}"
+REGEX="${PMC_REGEX:-gnca_k}"
+OUT="${PMC_OUT:-gpurun_out/pmc}"
+mkdir -p "$OUT"
 i=0
 while read -r counters; do
   [ -z "$counters" ] && continue
   i=$((i+1))
   echo "=== pass $i: $counters"
-  timeout -k 10 300 rocprofv3 --pmc $counters --kernel-include-regex "gnca_k" -d gpurun_out/pmc/p$i -o run --output-format csv -- $ARGS > gpurun_out/pmc/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $counters --kernel-include-regex "$REGEX" -d $OUT/p$i -o run --output-format csv -- $ARGS > $OUT/p$i.log 2>&1
   rc=$?
   echo "rc=$rc"
-  if [ $rc -ne 0 ]; then tail -20 gpurun_out/pmc/p$i.log; exit $rc; fi
+  if [ $rc -ne 0 ]; then tail -20 $OUT/p$i.log; exit $rc; fi
 done <<'LIST'
 FETCH_SIZE
 WRITE_SIZE

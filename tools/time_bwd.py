@@ -1,0 +1,78 @@
+"""Time the step forward and backward (C ABI) at a few sizes; prints one line per size.
+
+usage: python tools/time_bwd.py [--sizes 1024x72,16x40] [--iters 20]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import random
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from graph_neural_cellular_automata_amd import _lib as L  # noqa: E402
+from graph_neural_cellular_automata_amd import step as S  # noqa: E402
+from graph_neural_cellular_automata_amd.modules import NeuralCAGraph  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="1024x72,16x40")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--zp", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    model = NeuralCAGraph(16, 128, update_gain=0.05, alpha_thr=0.12, message_gain=0.25,
+                          graph_zero_padded_shift=args.zp).to(dev)
+    with torch.no_grad():
+        model.update_net[2].weight.normal_(0, 0.05)
+    tensors = dict(perception=model.perception.conv.weight, w1=model.update_net[0].weight,
+                   b1=model.update_net[0].bias, w2=model.update_net[2].weight,
+                   gn_weight=model.norm.weight, gn_bias=model.norm.bias)
+    tensors.update(model.graph.weight_tensors())
+    w, keep = S.make_weights(tensors)
+    want = {n: p for n, p in model.named_parameters() if n in S.GRAD_FIELDS}
+    random.seed(1)
+    chosen = random.sample(model.graph.offsets, 8)
+    flags = L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE | (L.ZERO_PAD_SHIFT if args.zp else 0)
+    for spec in args.sizes.split(","):
+        B, S_ = (int(v) for v in spec.split("x"))
+        x = torch.rand(B, 16, S_, S_, device=dev)
+        x[:, 4:] = torch.randn(B, 12, S_, S_, device=dev)
+        gy = torch.randn_like(x)
+        d = S.make_desc(B=B, C=16, H=S_, W=S_, hidden=128, d_model=16, offsets=chosen, flags=flags,
+                        update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                        fire_mode=L.FIRE_HASH, rng_seed=3)
+        for _ in range(3):
+            S.step(d, w, x)
+            S.step_backward(d, w, x, gy, want=want)
+        torch.cuda.synchronize()
+        ws = S.workspace(d, dev)
+        S.step(d, w, x, ws=ws)
+        e0, e1, e2, e3 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+        e0.record()
+        for _ in range(args.iters):
+            S.step(d, w, x, ws=ws)
+        e1.record()
+        for _ in range(args.iters):
+            S.step_backward(d, w, x, gy, want=want)
+        e2.record()
+        for _ in range(args.iters):
+            S.step_backward(d, w, x, gy, want=want, saved=ws)
+        e3.record()
+        torch.cuda.synchronize()
+        f = e0.elapsed_time(e1) / args.iters
+        b = e1.elapsed_time(e2) / args.iters
+        bs = e2.elapsed_time(e3) / args.iters
+        cells = B * S_ * S_
+        print(f"B={B} {S_}x{S_} zp={int(args.zp)}: fwd {f:.3f} ms  bwd(recompute) {b:.3f} ms  "
+              f"bwd(saved) {bs:.3f} ms  bwd/fwd {bs / f:.2f}  "
+              f"fwd+bwd {cells / ((f + bs) * 1e-3) / 1e9:.3f} G cell/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
