@@ -64,6 +64,12 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) on a node; gloo only to rehearse N>1 ranks on one GPU")
+    ap.add_argument("--mode", default="rollout", choices=["rollout", "train"],
+                    help="rollout: the BASELINE.json headline (default).  train: the graph "
+                         "trainer's BPTT iteration (SURVEY.md §8f rank 1), steps = iterations")
+    ap.add_argument("--train-batch", type=int, default=16, help="train: samples per GPU (config.json)")
+    ap.add_argument("--train-size", type=int, default=40, help="train: canvas (config.json img_size)")
+    ap.add_argument("--train-rollout", type=int, default=64, help="train: CA steps per iteration")
     return ap.parse_args()
 
 
@@ -140,6 +146,84 @@ def cpu_baseline(budget_s: float):
                       f"single-threaded; host CPU: {cpu}"}
 
 
+def main_train(args, dev, world, rank):
+    """One data-parallel BPTT iteration of the graph trainer (train_graph_augmented_nca.py:289-375):
+    rollout (fire rate ~ U(0.5, 0.9) per step, message every 3rd step), premultiplied-RGBA MSE,
+    loss.backward() through the HIP step, one flat RCCL gradient all-reduce, per-parameter grad
+    normalisation, Adam.  Weak scaling: ``--train-batch`` samples per GPU."""
+    import torch.distributed as dist
+    from graph_neural_cellular_automata_amd import NeuralCAGraph
+    from graph_neural_cellular_automata_amd.dp import allreduce_gradients, normalize_gradients_
+    torch.manual_seed(7 + rank)
+    random.seed(42)                       # identical offset draws / fire rates on every rank
+    model = NeuralCAGraph(C, HD, update_gain=GAIN, alpha_thr=THR, message_gain=MSG_GAIN,
+                          graph_d_model=D_MODEL, graph_attention_radius=R, graph_num_neighbors=K,
+                          graph_zero_padded_shift=False).to(dev)
+    sd = {k: v for k, v in load_weights(dev).items()}
+    model.load_state_dict(sd, strict=False)
+    opt = torch.optim.Adam(model.parameters(), lr=2e-4, weight_decay=1e-5)
+    params = [p for p in model.parameters() if p.requires_grad]
+    B, H, T = args.train_batch, args.train_size, args.train_rollout
+    g = torch.Generator(device=dev).manual_seed(99 + rank)
+    x0 = torch.rand(B, C, H, H, device=dev, generator=g)
+    x0[:, 4:] = torch.randn(B, C - 4, H, H, device=dev, generator=g)
+    target = torch.rand(4, H, H, device=dev, generator=g)
+    target[:3] *= target[3:4]
+
+    def iteration():
+        state = x0.clone()
+        for t in range(T):
+            fr = random.uniform(0.5, 0.9)
+            model.message_gain = MSG_GAIN if t % 3 == 0 else 0.0   # message_every = 3
+            state = model(state, fire_rate=fr)
+        model.message_gain = MSG_GAIN
+        rgba = torch.cat([state[:, :3] * state[:, 3:4], state[:, 3:4]], 1)
+        loss = ((rgba - target[None]) ** 2).mean()
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        allreduce_gradients(params)
+        normalize_gradients_(params)
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        iteration()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = iteration()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    if rank == 0:
+        cells = B * H * H * T * args.steps * world
+        line = {
+            "metric": "BPTT training cell-updates/sec (forward+backward through the CA step), "
+                      "graph trainer iteration",
+            "value": cells / el, "unit": "cell-updates/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic states and target; trained nca_latest.pt weights (golden fixture)",
+            "config": {"workload": f"graph trainer BPTT iteration: rollout {T} steps, fire U(0.5,0.9), "
+                                   f"message every 3rd step, premult-RGBA MSE, RCCL flat grad "
+                                   f"all-reduce, grad/||grad||, Adam", "channels": C, "hidden": HD,
+                       "height": H, "width": H, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"dp{world}"},
+            "iterations_per_s": args.steps / el, "final_loss": float(loss.detach()),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -154,6 +238,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    if args.mode == "train":
+        return main_train(args, dev, world, rank)
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
     lib = L.load()

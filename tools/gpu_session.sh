@@ -24,6 +24,8 @@ for s in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 96 --warmup 8 ;;
     benchq) run bench 600 python bench.py --steps 24 --warmup 4 --no-cpu ;;
+    train) run bench_train 600 python bench.py --mode train --steps 10 --warmup 2 ;;
+    train2) run bench_train2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --mode train --gpus 2 --steps 6 --warmup 2 --dist-backend gloo ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 24 --warmup 4 --no-cpu ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
