@@ -56,7 +56,7 @@ __device__ float g_zero[4];  // LDS-DMA source for off-image cells (zero-initial
 // LDS layout of K1 (floats; every region starts on a 16-byte boundary)
 // ------------------------------------------------------------------------------------------
 struct K1Layout {
-  int b1s, bms, percs, wts, kp_, red, wmf, w1f, w2f, sp, xs, al, total;
+  int b1s, bms, percs, wts, kp_, lst, red, wmf, w1f, w2f, sp, xs, al, total;
   int RH, RW, PSTR, NI, NIA, ALW;
 };
 
@@ -85,6 +85,7 @@ __host__ __device__ inline K1Layout k1_layout(int CP, int HDP, int TH, int TW, i
   L.sp = o; o += r4(L.RH * L.RW);
   L.al = o; o += 64 * L.NIA;
   L.kp_ = o; o += r4(TH * TW);              // per-tile keep plane (fire, then fire AND alive)
+  L.lst = o; o += r4(TH * TW) + 8;          // compacted live-cell list (ints) + per-wave counts
   L.b1s = o; o += r4(HDP);
   L.bms = o; o += r4(CP);
   L.percs = o; o += CP * 36;
@@ -185,6 +186,7 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
   const bool want_attn = FIXED ? false : (a.flags & GNCA_ATTENTION) != 0;
   const bool uniform_w = FIXED ? true : a.offw == nullptr;
+  const bool compact = !msg_only && !want_attn;   // skip cells whose update is masked to zero
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
 
   // ---- weights -> LDS in MFMA fragment order (once per persistent workgroup) ----
@@ -397,13 +399,51 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
     float amin = INFINITY, amax = -INFINITY;
     const size_t cell0 = (size_t)i0 * W + j0;
 
-    const int qend = FIXED ? cGPW * NW : ngroups;
+    // ---- live-cell compaction.  keep = pre-alive AND fire; a cell with keep == 0 has dx = 0
+    //      exactly (the reference multiplies its update by the masks, ncagraph.py:144-150), so
+    //      its MLP / message work is skipped and its zeros are stored here.  The live cells are
+    //      listed in cell order (wave ballots, fixed order: deterministic) and packed 16 per MFMA
+    //      group.  Off for the message-only and attention calls, which need every cell. ----
+    int* lst = reinterpret_cast<int*>(smem + L.lst);
+    int* wcnt = lst + r4(TH * TW);
+    int nlive = 0;
+    if (compact) {
+      for (int n0 = 0; n0 < ncell; n0 += kThreads) {
+        const int n = n0 + tid;
+        const int ti = n / TW, tj = n - (n / TW) * TW;
+        const bool inb = n < ncell && i0 + ti < H && j0 + tj < W;
+        const bool live = inb && fp[n] != 0.f;
+        const uint64_t bal = __ballot(live);
+        const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wcnt[wave] = __popcll(bal);
+        __syncthreads();
+        int off = nlive, tot = 0;
+        for (int w_ = 0; w_ < NW; ++w_) {
+          off += w_ < wave ? wcnt[w_] : 0;
+          tot += wcnt[w_];
+        }
+        if (live) {
+          lst[off + pre] = n;
+        } else if (inb) {
+          float* oz = a.out + (size_t)b * C * HW + cell0 + (size_t)ti * W + tj;
+          for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
+        }
+        nlive += tot;
+        __syncthreads();   // wcnt is rewritten by the next pass
+      }
+    }
+
+    const int qend = compact ? (nlive + 15) >> 4 : (FIXED ? cGPW * NW : ngroups);
 #pragma unroll 1
     for (int q = wave; q < qend; q += NW) {
-      const int n = 16 * q + c16;
-      int ti = n / TW, tj = n - (n / TW) * TW;
+      int n = 16 * q + c16;
       bool valid = true;
-      if constexpr (!FIXED) {
+      if (compact) {
+        valid = n < nlive;
+        n = lst[valid ? n : 0];
+      }
+      int ti = n / TW, tj = n - (n / TW) * TW;
+      if (!FIXED && !compact) {
         valid = n < ncell && i0 + ti < H && j0 + tj < W;
         if (!valid) { ti = 0; tj = 0; }
       }
@@ -595,7 +635,7 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
       }
 
       // -- epilogue: dx = (dl + tanh(m)*message_gain) * keep, keep = pre-alive AND fire --
-      const float keep = fp[valid ? n : 0];
+      const float keep = valid ? fp[n] : 0.f;
       float* ob = a.out + ((size_t)b * C + 4 * g) * HW + cell0;
 #pragma unroll
       for (int mo = 0; mo < MO; ++mo)
