@@ -313,13 +313,23 @@ def main():
     torch.cuda.synchronize()
     k1_ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(reps))[reps // 2]
     k2_ms = sorted(ev2[2 * r].elapsed_time(ev2[2 * r + 1]) for r in range(reps))[reps // 2]
+    # live fraction of this K1 launch: cells with keep = pre-alive AND fire (the others have
+    # dx = 0 exactly and K1 skips their MLP work; the algorithmic count stays dense, per cell)
+    fm = S.fire_mask(d, dev)
+    alive = torch.nn.functional.max_pool2d(out[:, 3:4], 3, 1, 1) > THR
+    live_frac = float((alive & (fm != 0)).float().mean())
     k1_flops = cells * FLOP_PER_CELL
     k2_bytes = cells * C * 4 * 3                   # read x, dx; write x'
     roof = {"bound": "mfma", "kernel": "gnca_k1_update<16,128>", "achieved": k1_flops / (k1_ms * 1e-3) / 1e12,
             "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
             "frac": k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA, "traffic": pmc_traffic("K1"),
             "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, profiles/r01_pmc_traffic.json)",
-            "k1_ms": k1_ms, "flop_per_launch": k1_flops}
+            "k1_ms": k1_ms, "flop_per_launch": k1_flops,
+            "live_fraction": live_frac,
+            "executed_frac": live_frac * k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA,
+            "note": "achieved = dense algorithmic FLOPs (16,896 per cell-update, SURVEY.md 8d) / K1 "
+                    "time; K1 executes the MLP only for live cells (keep = alive AND fire, the "
+                    "others have dx = 0 exactly), so MFMA utilisation = executed_frac"}
     roof_k2 = {"bound": "hbm", "kernel": "gnca_k2_finalize", "achieved": k2_bytes / (k2_ms * 1e-3) / 1e9,
                "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": k2_bytes / (k2_ms * 1e-3) / PEAK_HBM,
                "k2_ms": k2_ms, "bytes_per_launch": k2_bytes, "traffic": pmc_traffic("K2")}

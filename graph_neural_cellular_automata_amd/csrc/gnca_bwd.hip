@@ -45,6 +45,7 @@ namespace gnca {
 namespace {
 
 constexpr int NW = kThreads / 64;
+__device__ float g_bzero[4];   // LDS-DMA source for off-image cells (zero-initialised)
 constexpr uint32_t kMsg = 1u << 16;      // message path active (k > 0 and message_gain != 0)
 constexpr uint32_t kFirst = 1u << 17;    // first hidden slice: also the message backward
 constexpr uint32_t kGN = 1u << 18;       // GroupNorm on
@@ -221,16 +222,18 @@ __global__ __launch_bounds__(kThreads) void gnca_b_coef(const double* stats, con
 // BB: the MFMA kernel
 // ------------------------------------------------------------------------------------------
 struct BBLayout {
-  int xs, PSTR, al, ALW, sp, kp, w1f, KSP, w1t, S1T, w2t, S2T, wms, SWM, b1s, bms, percs, wts, scr;
-  int ST1, ST2, ST3, SCRW, RH, RW, total;
+  int xs, PSTR, al, ALW, sp, kp, lst, w1f, KSP, w1t, S1T, w2t, S2T, wms, SWM, b1s, bms, percs, wts, scr;
+  int ST1, ST2, ST3, SCRW, RH, RW, NI, NIA, total;
 };
 
 __host__ __device__ inline BBLayout bb_layout(int CP, int HB, int TH, int TW, int RY, int RX, int kmax) {
   BBLayout L;
   L.RH = TH + 2 * RY;
   L.RW = TW + 2 * RX;
-  L.PSTR = r4(L.RH * L.RW);
+  L.NI = (L.RH * L.RW + 63) / 64;          // LDS-DMA wave instructions per channel plane
+  L.PSTR = 64 * L.NI + 16;
   L.ALW = L.RW + 2;
+  L.NIA = ((L.RH + 2) * L.ALW + 63) / 64;
   const int CPM = 16 * ((CP + 15) / 16);   // channel rows padded to whole 16-row MFMA tiles
   const int MT = HB / 16, MO = (CP + 15) / 16, FT = (3 * CP + 15) / 16;
   L.KSP = odd4(3 * CP / 4);   // MFMA A-fragments, one 16-byte LDS read per 4 k-steps (as K1)
@@ -243,9 +246,10 @@ __host__ __device__ inline BBLayout bb_layout(int CP, int HB, int TH, int TW, in
   L.SCRW = 16 * (L.ST1 + std::max(L.ST2, 2 * L.ST3));   // T3/T4 reuse T2's rows (after dW1)
   int o = 0;
   L.xs = o; o += CP * L.PSTR;
-  L.al = o; o += r4((L.RH + 2) * L.ALW);
+  L.al = o; o += 64 * L.NIA;
   L.sp = o; o += r4(L.RH * L.RW);
   L.kp = o; o += r4(TH * TW);
+  L.lst = o; o += r4(TH * TW) + 8;   // compacted live-cell list + per-wave counts
   L.w1f = o; o += MT * 64 * L.KSP;   // W1 fragments (GEMM1 recompute)
   L.w1t = o; o += FT * 64 * L.S1T;   // W1^T fragments (dY = W1^T dh)
   L.w2t = o; o += MT * 64 * L.S2T;   // W2^T fragments (dh = W2^T d_pre)
@@ -416,64 +420,136 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     float* dYb = a.dY + (size_t)b * 3 * C * HW;
     float* dGb = a.dG + (size_t)b * C * HW;
     __syncthreads();
-    // ---- staging: channel planes over the (RH x RW) region, alpha with one more ring ----
-    for (int e = tid; e < CP * RH * RW; e += kThreads) {
-      const int c = e / (RH * RW), pos = e - c * (RH * RW);
-      const int vr = pos / RW, vc = pos - vr * RW;
-      int ii = i0 - RY + vr, jj = j0 - RX + vc;
+    // ---- staging by LDS-DMA (as the forward K1): every channel plane of the (RH x RW) region
+    //      and the alpha plane with one more ring, all loads in flight at once, no VGPR round
+    //      trip; torus-wrapped, or a zero source outside the image in pad mode ----
+    for (int ii_ = wave; ii_ < L.NI; ii_ += NW) {
+      const int e = 64 * ii_ + lane;
+      int off = 0;
       bool ok = true;
-      if (zp) ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
-      else { ii = wrapi(ii, H); jj = wrapi(jj, W); }
-      xs[c * PSTR + pos] = (ok && c < C) ? xb[(size_t)c * HW + (size_t)ii * W + jj] : 0.f;
+      if (e < RH * RW) {
+        const int vr = e / RW, vc = e - (e / RW) * RW;
+        int ii = i0 - RY + vr, jj = j0 - RX + vc;
+        if (zp) {
+          ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
+          off = ok ? ii * W + jj : 0;
+        } else {
+          while (ii < 0) ii += H; while (ii >= H) ii -= H;
+          while (jj < 0) jj += W; while (jj >= W) jj -= W;
+          off = ii * W + jj;
+        }
+      }
+      float* dst = xs + 64 * ii_;
+      for (int c = 0; c < CP; ++c) {
+        const float* src = xb + (size_t)min(c, C - 1) * HW + off;
+        if ((zp && !ok) || c >= C) src = g_bzero;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(dst + c * PSTR), 4, 0, 0);
+      }
     }
-    for (int e = tid; e < (RH + 2) * ALW; e += kThreads) {
-      const int vr = e / ALW, vc = e - vr * ALW;
-      int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
+    for (int ii_ = wave; ii_ < L.NIA; ii_ += NW) {
+      const int e = 64 * ii_ + lane;
+      int off = 0;
       bool ok = true;
-      if (zp) ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
-      else { ii = wrapi(ii, H); jj = wrapi(jj, W); }
-      al[e] = ok ? xb[3 * HW + (size_t)ii * W + jj] : 0.f;
+      if (e < (RH + 2) * ALW) {
+        const int vr = e / ALW, vc = e - (e / ALW) * ALW;
+        int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
+        if (zp) {
+          ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
+          off = ok ? ii * W + jj : 0;
+        } else {
+          while (ii < 0) ii += H; while (ii >= H) ii -= H;
+          while (jj < 0) jj += W; while (jj >= W) jj -= W;
+          off = ii * W + jj;
+        }
+      }
+      const float* src = (zp && !ok) ? g_bzero : xb + 3 * HW + off;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(al + 64 * ii_), 4, 0, 0);
     }
     if (msg && !uniform_w)
       for (int o = tid; o < k; o += kThreads) wts[o] = a.offw[(size_t)b * k + o];
-    for (int n = tid; n < ncell; n += kThreads) {
-      const int ti = n / TW, tj = n - (n / TW) * TW;
-      const int i = min(i0 + ti, H - 1), j = min(j0 + tj, W - 1);
-      fp[n] = fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step, a.sample_base, b, HW,
-                      (size_t)i * W + j) ? 1.f : 0.f;
+    for (int ti = wave; ti < TH; ti += NW) {
+      if (lane < TW) {
+        const int i = min(i0 + ti, H - 1), j = min(j0 + lane, W - 1);
+        fp[ti * TW + lane] = fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step,
+                                     a.sample_base, b, HW, (size_t)i * W + j) ? 1.f : 0.f;
+      }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // ---- sender plane over the region, keep = pre-alive AND fire on the tile (as K1) ----
-    for (int pos = tid; pos < RH * RW; pos += kThreads) {
-      const int vr = pos / RW, vc = pos - vr * RW;
-      int iq = i0 - RY + vr, jq = j0 - RX + vc;
-      bool in_img = true;
-      if (zp) in_img = iq >= 0 && iq < H && jq >= 0 && jq < W;
-      else { iq = wrapi(iq, H); jq = wrapi(jq, W); }
-      const float* q = al + (vr + 1) * ALW + (vc + 1);
-      const float NEG = -INFINITY;
-      const bool up = iq > 0, dn = iq < H - 1, lf = jq > 0, rt = jq < W - 1;
-      const float mu_ = fmaxf(fmaxf(lf ? q[-ALW - 1] : NEG, q[-ALW]), rt ? q[-ALW + 1] : NEG);
-      const float mm_ = fmaxf(fmaxf(lf ? q[-1] : NEG, q[0]), rt ? q[1] : NEG);
-      const float md_ = fmaxf(fmaxf(lf ? q[ALW - 1] : NEG, q[ALW]), rt ? q[ALW + 1] : NEG);
-      const float mx = fmaxf(fmaxf(up ? mu_ : NEG, mm_), dn ? md_ : NEG);
-      sp[pos] = a2a ? ((in_img && mx > gthr) ? 1.f : 0.f) : (in_img ? 1.f : 0.f);
-      const int ti = vr - RY, tj = vc - RX;
-      if (ti >= 0 && ti < TH && tj >= 0 && tj < TW) {
-        const int n = ti * TW + tj;
-        fp[n] = (in_img && mx > thr) ? fp[n] : 0.f;
+    {
+      int jq = j0 - RX + lane;
+      bool inc = true;
+      if (zp) inc = jq >= 0 && jq < W;
+      else { while (jq < 0) jq += W; while (jq >= W) jq -= W; }
+      const bool lf = jq > 0, rt = jq < W - 1;
+      for (int vr = wave; vr < RH; vr += NW) {
+        if (lane >= RW) continue;
+        const int vc = lane;
+        int iq = i0 - RY + vr;
+        bool in_img = inc;
+        if (zp) in_img = in_img && iq >= 0 && iq < H;
+        else { while (iq < 0) iq += H; while (iq >= H) iq -= H; }
+        const float* q = al + (vr + 1) * ALW + (vc + 1);
+        const float NEG = -INFINITY;
+        const bool up = iq > 0, dn = iq < H - 1;
+        const float mu_ = fmaxf(fmaxf(lf ? q[-ALW - 1] : NEG, q[-ALW]), rt ? q[-ALW + 1] : NEG);
+        const float mm_ = fmaxf(fmaxf(lf ? q[-1] : NEG, q[0]), rt ? q[1] : NEG);
+        const float md_ = fmaxf(fmaxf(lf ? q[ALW - 1] : NEG, q[ALW]), rt ? q[ALW + 1] : NEG);
+        const float mx = fmaxf(fmaxf(up ? mu_ : NEG, mm_), dn ? md_ : NEG);
+        const int pos = vr * RW + vc;
+        sp[pos] = a2a ? ((in_img && mx > gthr) ? 1.f : 0.f) : (in_img ? 1.f : 0.f);
+        const int ti = vr - RY, tj = vc - RX;
+        if (ti >= 0 && ti < TH && tj >= 0 && tj < TW) {
+          const int n = ti * TW + tj;
+          fp[n] = (in_img && mx > thr) ? fp[n] : 0.f;
+        }
       }
     }
     __syncthreads();
     const float mu = a.coef[4 * b], rs = a.coef[4 * b + 1];
     const float mu_u = a.coef[4 * b + 2], mu_ux = a.coef[4 * b + 3];
+    // ---- live-cell compaction (as the forward K1): a cell with keep == 0 has d_pre = 0, so its
+    //      dY / dG are zero and it adds nothing to any weight gradient; only live cells are
+    //      packed into MFMA groups, the zeros of the dead ones are stored here ----
+    int* lst = reinterpret_cast<int*>(smem + L.lst);
+    int* wcnt = lst + r4(TH * TW);
+    int nlive = 0;
+    for (int n0 = 0; n0 < ncell; n0 += kThreads) {
+      const int n = n0 + tid;
+      const int ti = n / TW, tj = n - (n / TW) * TW;
+      const bool inb = n < ncell && i0 + ti < H && j0 + tj < W;
+      const bool live = inb && fp[n] != 0.f;
+      const uint64_t bal = __ballot(live);
+      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) wcnt[wave] = __popcll(bal);
+      __syncthreads();
+      int off = nlive, tot = 0;
+      for (int w_ = 0; w_ < NW; ++w_) {
+        off += w_ < wave ? wcnt[w_] : 0;
+        tot += wcnt[w_];
+      }
+      if (live) {
+        lst[off + pre] = n;
+      } else if (inb && first) {
+        const int ce = (i0 + ti) * W + (j0 + tj);
+        for (int pl = 0; pl < 3 * C; ++pl) dYb[pl * HWi + ce] = 0.f;
+        if (msg)
+          for (int c = 0; c < C; ++c) dGb[c * HWi + ce] = 0.f;
+        if (a.dmb) a.dmb[(size_t)b * HW + ce] = 0.f;
+      }
+      nlive += tot;
+      __syncthreads();
+    }
 
 #pragma unroll 1
-    for (int q = wave; q < ngroups; q += NW) {
-      const int n = 16 * q + c16;
-      int ti = n / TW, tj = n - (n / TW) * TW;
-      const bool valid = n < ncell && i0 + ti < H && j0 + tj < W;
-      if (!valid) { ti = 0; tj = 0; }
+    for (int q = wave; q < ((nlive + 15) >> 4); q += NW) {
+      const int idx = 16 * q + c16;
+      const bool valid = idx < nlive;
+      const int n = lst[valid ? idx : 0];
+      const int ti = n / TW, tj = n - (n / TW) * TW;
       const int pidx = (RY + ti) * RW + (RX + tj);
       const int celli = (i0 + ti) * W + (j0 + tj);
       const float* xg = xs + g * PSTR;
@@ -1263,7 +1339,7 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
     const int padh = ns * v.HB - Hd;
     for (int th : ths)
       for (int tw : tws) {
-        if ((th * tw) % 64) continue;
+        if ((th * tw) % 64 || tw + 2 * rx + 2 > 64) continue;   // staging rows fit one wave
         const BBLayout L = bb_layout(P->CP, v.HB, th, tw, ry, rx, P->F.k);
         const size_t bytes = (size_t)L.total * 4;
         if (bytes > 160 * 1024) continue;

@@ -973,6 +973,16 @@ __global__ __launch_bounds__(kThreads) void gnca_perceive(int B, int C, int H, i
   }
 }
 
+// The GNCA_FIRE_HASH mask as uint8 (gnca_fire_mask_u8)
+__global__ __launch_bounds__(kThreads) void gnca_fire_mask(uint8_t* mask, int B, int HW, uint64_t seed,
+                                                           int64_t step, int64_t sample_base, float rate) {
+  const size_t total = (size_t)B * HW;
+  for (size_t e = (size_t)blockIdx.x * kThreads + threadIdx.x; e < total; e += (size_t)gridDim.x * kThreads) {
+    const size_t b = e / HW, cell = e - b * HW;
+    mask[e] = hash_uniform(seed, step, (uint64_t)(sample_base + (int64_t)b), cell) <= rate ? 1 : 0;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
@@ -1383,6 +1393,17 @@ int gnca_perceive_f32(int32_t B, int32_t C, int32_t H, int32_t W, const float* w
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(gnca_perceive, dim3((unsigned)blocks), dim3(kThreads), 0,
                      reinterpret_cast<hipStream_t>(stream), B, C, H, W, weight, x, y);
+  return check_launch();
+}
+
+int gnca_fire_mask_u8(const gnca_step_desc* desc, uint8_t* mask, void* stream) {
+  if (!desc || !mask || desc->B <= 0 || desc->H <= 0 || desc->W <= 0) return GNCA_ERR_INVALID;
+  const size_t total = (size_t)desc->B * desc->H * desc->W;
+  size_t blocks = (total + kThreads - 1) / kThreads;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(gnca_fire_mask, dim3((unsigned)blocks), dim3(kThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), mask, desc->B, desc->H * desc->W,
+                     desc->rng_seed, desc->rng_step, desc->sample_base, desc->fire_rate);
   return check_launch();
 }
 

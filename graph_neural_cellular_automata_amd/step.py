@@ -130,6 +130,14 @@ def perceive(weight, x):
     return y
 
 
+def fire_mask(desc, device) -> torch.Tensor:
+    """The [B,1,H,W] uint8 fire mask a GNCA_FIRE_HASH step with ``desc`` draws."""
+    m = torch.empty(desc.B, 1, desc.H, desc.W, dtype=torch.uint8, device=device)
+    L.check(L.load().gnca_fire_mask_u8(ctypes.byref(desc), m.data_ptr(), stream_ptr(device)),
+            "gnca_fire_mask_u8")
+    return m
+
+
 def rollout(desc, weights, x, steps: int, offsets_per_step: list):
     """``steps`` no-grad steps (GNCA_FIRE_HASH / NONE) in one C call."""
     lib = L.load()

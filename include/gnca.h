@@ -156,6 +156,13 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
                      const int8_t* offsets, const float* x, float* x_final, float* scratch,
                      void* ws, size_t ws_bytes, void* stream);
 
+/*
+ * The fire mask a GNCA_FIRE_HASH step would draw: mask[b,0,i,j] = u(rng_seed, rng_step,
+ * sample_base+b, i*W+j) <= fire_rate, as uint8 [B,1,H,W] (1 = fires).  For inspection and for
+ * replaying a hash-masked rollout elsewhere (e.g. as GNCA_FIRE_MASK_U8).
+ */
+int gnca_fire_mask_u8(const gnca_step_desc* desc, uint8_t* mask, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Backward (BPTT).  Gradients of one step, written into caller buffers (overwritten, not
  * accumulated), in the reference's parameter layouts.  A NULL pointer skips that gradient's

@@ -169,3 +169,16 @@ def test_long_rollout_drift(dev):
         ref = O.nca_step(ref, p, cfg, chosen=offs[t], fire_mask=O.hash_fire_mask(5, t, 0, 2, 32, 32, 0.5))
     assert np.abs(got - ref).max() <= 1e-4
     np.testing.assert_array_equal(O.alive_mask(got, 0.12), O.alive_mask(ref, 0.12))
+
+
+def test_fire_mask_u8_matches_oracle_hash(dev):
+    """gnca_fire_mask_u8 materialises exactly the oracle's counter-RNG fire mask (with an offset
+    sample_base and a later rng_step)."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    d = S.make_desc(B=3, C=16, H=20, W=33, hidden=128, d_model=16, offsets=[], flags=L.GRAPH,
+                    update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.37,
+                    fire_mode=L.FIRE_HASH, rng_seed=123456789, rng_step=17, sample_base=1000)
+    m = S.fire_mask(d, dev).cpu().numpy()
+    ref = O.hash_fire_mask(123456789, 17, 1000, 3, 20, 33, 0.37)
+    np.testing.assert_array_equal(m.astype(np.float32), ref)
