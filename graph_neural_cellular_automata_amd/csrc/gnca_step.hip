@@ -28,6 +28,8 @@
 // so each lane computes its own perception features.  GEMM1's accumulator rows (hidden 4g+r of
 // tile m) are exactly the B operand of GEMM2 DL = W2 H at k-step (m, r) — no data movement.
 
+#include <stdlib.h>
+
 #include <mutex>
 #include <type_traits>
 #include <unordered_map>
@@ -90,7 +92,7 @@ __host__ __device__ inline K1Layout k1_layout(int CP, int HDP, int TH, int TW, i
   L.bms = o; o += r4(CP);
   L.percs = o; o += CP * 36;
   L.wts = o; o += kp;
-  L.red = o; o += 32;
+  L.red = o; o += 64;                     // per-wave partials (up to 8 waves)
   L.wmf = o; o += MO * 64 * SWM;
   L.w2f = o; o += MO * 64 * S2;
   L.w1f = o; o += MT * 64 * KSP;
@@ -135,8 +137,8 @@ __device__ __forceinline__ float fast_tanh(float x) {
 // specialised instantiations (every LDS offset becomes an instruction immediate); 0 = runtime.
 // fp32 MFMA shares the SIMD's fp32 datapath with VALU on gfx950 (profiles/r01_ubench_*), so the
 // body is written to minimise VALU instructions per 16-cell group.
-template <int CP, int HDP, int TH_, int TW_, int RY_, int RX_, int KU_>
-__global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
+template <int CP, int HDP, int TH_, int TW_, int RY_, int RX_, int KU_, int NT = kThreads>
+__global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CPQ = CP / 4, KS = 3 * CPQ, MT = HDP / 16, MO = (CP + 15) / 16;
   constexpr int KSP = ((((KS + 3) & ~3) >> 2) & 1) ? ((KS + 3) & ~3) : ((KS + 3) & ~3) + 4;
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   constexpr int S2 = ((S2r >> 2) & 1) ? S2r : S2r + 4;
   constexpr int SWMr = (CPQ + 3) & ~3;
   constexpr int SWM = ((SWMr >> 2) & 1) ? SWMr : SWMr + 4;
-  constexpr int NW = kThreads / 64;
+  constexpr int NW = NT / 64;
   constexpr bool W1REG = w1_in_regs(CP, HDP);
   constexpr bool W2REG = false;   // W2 fragments are read from LDS right before GEMM2
   constexpr bool FIXED = TH_ > 0;
@@ -152,8 +154,8 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
   constexpr int cRH = TH_ + 2 * RY_, cRW = TW_ + 2 * RX_;
   constexpr int cNI = (cRH * cRW + 63) / 64, cPSTR = 64 * cNI + 16;
   constexpr int cALW = cRW + 2, cNIA = ((cRH + 2) * cALW + 63) / 64;
-  constexpr int cGPW = (TH_ * TW_ / 16) / NW;   // groups per wave per tile (fixed geometry)
-  static_assert(!FIXED || (TH_ * TW_) % (16 * NW) == 0, "fixed tiles hold whole groups per wave");
+  constexpr int cGPW = (TH_ * TW_ / 16 + NW - 1) / NW;   // groups per wave per tile (fixed geometry)
+  static_assert(!FIXED || (TH_ * TW_) % 16 == 0, "fixed tiles hold whole 16-cell groups");
 
   const int TH = FIXED ? TH_ : a.TH, TW = FIXED ? TW_ : a.TW;
   const int RY = FIXED ? RY_ : a.RY, RX = FIXED ? RX_ : a.RX;
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
 
   // ---- weights -> LDS in MFMA fragment order (once per persistent workgroup) ----
   if (!msg_only) {
-    for (int idx = tid; idx < MT * 64 * KSP; idx += kThreads) {
+    for (int idx = tid; idx < MT * 64 * KSP; idx += NT) {
       const int s = idx % KSP, ml = idx / KSP, l = ml & 63, m = ml >> 6;
       const int hid = 16 * m + (l & 15), slot = 4 * s + (l >> 4);
       const int f = slot / CP, c = slot - f * CP;
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
       if (s < KS && hid < Hd && c < C) v = a.w1[(size_t)hid * 3 * C + f * C + c];
       w1f[idx] = v;
     }
-    for (int idx = tid; idx < MO * 64 * S2; idx += kThreads) {
+    for (int idx = tid; idx < MO * 64 * S2; idx += NT) {
       const int e = idx % S2, ml = idx / S2, l = ml & 63, mo = ml >> 6;
       const int m = e >> 2, r = e & 3;
       const int co = 16 * mo + (l & 15), hid = 16 * m + 4 * (l >> 4) + r;
@@ -207,25 +209,25 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
       if (e < S2r && co < C && hid < Hd) v = a.w2[(size_t)co * Hd + hid];
       w2f[idx] = v;
     }
-    for (int idx = tid; idx < HDP; idx += kThreads) b1s[idx] = idx < Hd ? a.b1[idx] : 0.f;
-    for (int idx = tid; idx < CP * 36; idx += kThreads) {
+    for (int idx = tid; idx < HDP; idx += NT) b1s[idx] = idx < Hd ? a.b1[idx] : 0.f;
+    for (int idx = tid; idx < CP * 36; idx += NT) {
       const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
       percs[idx] = (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
     }
   }
-  for (int idx = tid; idx < MO * 64 * SWM; idx += kThreads) {
+  for (int idx = tid; idx < MO * 64 * SWM; idx += NT) {
     const int s = idx % SWM, ml = idx / SWM, l = ml & 63, mo = ml >> 6;
     const int co = 16 * mo + (l & 15), c = 4 * s + (l >> 4);
     wmf[idx] = (graph_on && s < CPQ && co < C && c < C) ? a.wm[co * C + c] : 0.f;
   }
-  for (int idx = tid; idx < CP; idx += kThreads) bms[idx] = (graph_on && idx < C) ? a.bm[idx] : 0.f;
+  for (int idx = tid; idx < CP; idx += NT) bms[idx] = (graph_on && idx < C) ? a.bm[idx] : 0.f;
   __syncthreads();
 
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch)
   bool sobel = false;
   if (!msg_only) {
     int ok = 1;
-    for (int idx = tid; idx < C * 27; idx += kThreads) {
+    for (int idx = tid; idx < C * 27; idx += NT) {
       const int c = idx / 27, e = idx % 27, f = e / 9, tap = e % 9;
       const int tr = tap / 3, tc = tap % 3;
       float ref;
@@ -343,10 +345,10 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
     }
     // ---- per-tile side tables while the DMA is in flight: offset weights, fire plane ----
     if (graph_on && !uniform_w)
-      for (int o = tid; o < kp; o += kThreads)
+      for (int o = tid; o < kp; o += NT)
         wts[o] = o >= k ? 0.f : a.offw[(size_t)b * k + o];
 #pragma unroll 1
-    for (int n = tid; n < ncell; n += kThreads) {
+    for (int n = tid; n < ncell; n += NT) {
       const int ti = n / TW, tj = n - (n / TW) * TW;
       const int i = min(i0 + ti, H - 1), j = min(j0 + tj, W - 1);
       const size_t cell = (size_t)i * W + j;
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
     //      (alive_to_alive ? A_graph : 1, zero where the source is off-image) over the region, and
     //      keep = pre-update alive AND fire for the tile cells ----
 #pragma unroll 1
-    for (int pos = tid; pos < ((GNCA_ABLATE & kAblPlanes) ? 0 : RH * RW); pos += kThreads) {
+    for (int pos = tid; pos < ((GNCA_ABLATE & kAblPlanes) ? 0 : RH * RW); pos += NT) {
       const int vr = pos / RW, vc = pos - (pos / RW) * RW;
       int iq = i0 - RY + vr, jq = j0 - RX + vc;
       bool in_img = true;
@@ -408,7 +410,7 @@ __global__ __launch_bounds__(kThreads, 2) void gnca_k1_update(const K1Args a) {
     int* wcnt = lst + r4(TH * TW);
     int nlive = 0;
     if (compact) {
-      for (int n0 = 0; n0 < ncell; n0 += kThreads) {
+      for (int n0 = 0; n0 < ncell; n0 += NT) {
         const int n = n0 + tid;
         const int ti = n / TW, tj = n - (n / TW) * TW;
         const bool inb = n < ncell && i0 + ti < H && j0 + tj < W;
@@ -991,15 +993,17 @@ thread_local int g_last_hip = 0;
 struct Variant {
   int CP, HDP, TH, TW, RY, RX, KU;   // TH == 0: runtime geometry (generic)
   const void* fn;
+  int NT;                            // threads per workgroup
 };
 
-#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>)}
-#define GNCA_FV(cp, hd, th, tw, ry, rx, ku) \
-  {cp, hd, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, th, tw, ry, rx, ku>)}
+#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads}
+#define GNCA_FV(cp, hd, th, tw, ry, rx, ku, nt) \
+  {cp, hd, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, th, tw, ry, rx, ku, nt>), nt}
 static const Variant kVariants[] = {
     // compile-time geometry: the benchmark / trainer shapes (16 ch, hidden 128, 8x24 tiles)
-    GNCA_FV(16, 128, 8, 24, 4, 4, 8),   // graph, torus, r <= 4, K = 8
-    GNCA_FV(16, 128, 8, 24, 1, 1, 0),   // classic NCA (no gather)
+    GNCA_FV(16, 128, 24, 24, 4, 4, 8, 512),   // graph, torus, r <= 4, K = 8: 8 waves, 1 WG / CU
+    GNCA_FV(16, 128, 8, 24, 4, 4, 8, 256),    // same, 8x24 tiles, 2 WGs / CU
+    GNCA_FV(16, 128, 8, 24, 1, 1, 0, 256),    // classic NCA (no gather)
     // runtime geometry: every other shape class
     GNCA_GV(4, 32),   GNCA_GV(4, 64),   GNCA_GV(4, 128),  GNCA_GV(8, 32),   GNCA_GV(8, 64),
     GNCA_GV(8, 128),  GNCA_GV(12, 64),  GNCA_GV(12, 128), GNCA_GV(16, 32),  GNCA_GV(16, 64),
@@ -1055,12 +1059,15 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   const int CP = P->var->CP, HDP = P->var->HDP;
   const bool attn_on = attn && P->graph_on;
   // a compile-time-geometry instantiation, when the shape allows one
+  static const bool only256 = getenv("GNCA_K1_NT256") != nullptr;   // measurement knob (A/B)
   for (const Variant& v : kVariants) {
     if (v.TH == 0 || v.CP != CP || v.HDP != HDP || d->C != CP || msg_only || attn_on) continue;
+    if (only256 && v.NT > kThreads) continue;
     if (d->H % v.TH || d->W % v.TW || ry > v.RY || rx > v.RX) continue;
     if (v.KU > 0 ? !(P->graph_on && !zp && !P->need_k0 && P->k == v.KU) : P->graph_on) continue;
     const K1Layout L = k1_layout(CP, HDP, v.TH, v.TW, v.RY, v.RX, P->k);
-    if ((size_t)L.total * 4 > 80 * 1024) continue;
+    // LDS per workgroup: 80 KB for two 256-thread workgroups per CU, 160 KB for one of 512
+    if ((size_t)L.total * 4 > (v.NT >= 512 ? (size_t)max_lds_bytes() : 80 * 1024)) continue;
     P->var = &v;
     P->RY = v.RY;
     P->RX = v.RX;
@@ -1162,7 +1169,7 @@ static int device_cus() {
   return cus;
 }
 
-static int occupancy(const void* fn, size_t lds) {
+static int occupancy(const void* fn, size_t lds, int nt = kThreads) {
   static std::mutex mu;
   static std::unordered_map<const void*, std::unordered_map<size_t, int>> cache;
   std::lock_guard<std::mutex> lk(mu);
@@ -1171,7 +1178,7 @@ static int occupancy(const void* fn, size_t lds) {
   if (it != m.end()) return it->second;
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, lds) != hipSuccess || n <= 0) n = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, nt, lds) != hipSuccess || n <= 0) n = 1;
   if (n > 8) n = 8;
   m[lds] = n;
   return n;
@@ -1241,12 +1248,12 @@ static int launch_k0(const gnca_step_desc* d, const gnca_weights* w, const Plan&
 }
 
 static int launch_k1(const K1Args& k1, const Plan& P, hipStream_t st) {
-  const int occ = occupancy(P.var->fn, P.lds1);
+  const int occ = occupancy(P.var->fn, P.lds1, P.var->NT);
   long grid = (long)device_cus() * occ;
   if (grid > P.total_tiles) grid = P.total_tiles;
   if (grid < 1) grid = 1;
   void* args[] = {const_cast<K1Args*>(&k1)};
-  const hipError_t e = hipLaunchKernel(P.var->fn, dim3((unsigned)grid), dim3(kThreads), args, P.lds1, st);
+  const hipError_t e = hipLaunchKernel(P.var->fn, dim3((unsigned)grid), dim3(P.var->NT), args, P.lds1, st);
   if (e != hipSuccess) {
     g_last_hip = (int)e;
     return GNCA_ERR_HIP;
