@@ -28,6 +28,7 @@
 // so each lane computes its own perception features.  GEMM1's accumulator rows (hidden 4g+r of
 // tile m) are exactly the B operand of GEMM2 DL = W2 H at k-step (m, r) — no data movement.
 
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <mutex>
@@ -1001,7 +1002,12 @@ struct Variant {
   {cp, hd, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, th, tw, ry, rx, ku, nt>), nt}
 static const Variant kVariants[] = {
     // compile-time geometry: the benchmark / trainer shapes (16 ch, hidden 128, 8x24 tiles)
-    GNCA_FV(16, 128, 24, 24, 4, 4, 8, 512),   // graph, torus, r <= 4, K = 8: 8 waves, 1 WG / CU
+    // graph, torus, r <= 4, K = 8 (the benchmark / trainer shape class): one 512-thread workgroup
+    // per CU (8 waves share one copy of the weight fragments), the largest tiles whose halo fits
+    // LDS (24x36: 1.6x halo re-read; measured 24x24 0.72 ms, 24x36 0.68 ms per B=1024 72^2 launch)
+    GNCA_FV(16, 128, 24, 36, 4, 4, 8, 512),
+    GNCA_FV(16, 128, 36, 24, 4, 4, 8, 512),
+    GNCA_FV(16, 128, 24, 24, 4, 4, 8, 512),
     GNCA_FV(16, 128, 8, 24, 4, 4, 8, 256),    // same, 8x24 tiles, 2 WGs / CU
     GNCA_FV(16, 128, 8, 24, 1, 1, 0, 256),    // classic NCA (no gather)
     // runtime geometry: every other shape class
@@ -1059,10 +1065,17 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   const int CP = P->var->CP, HDP = P->var->HDP;
   const bool attn_on = attn && P->graph_on;
   // a compile-time-geometry instantiation, when the shape allows one
-  static const bool only256 = getenv("GNCA_K1_NT256") != nullptr;   // measurement knob (A/B)
+  // measurement knobs (A/B runs only): GNCA_K1_NT256 skips the 512-thread variants,
+  // GNCA_K1_TILE=<TH>x<TW> restricts the fixed variants to one tile shape
+  static const bool only256 = getenv("GNCA_K1_NT256") != nullptr;
+  static const char* tile_env = getenv("GNCA_K1_TILE");
   for (const Variant& v : kVariants) {
     if (v.TH == 0 || v.CP != CP || v.HDP != HDP || d->C != CP || msg_only || attn_on) continue;
     if (only256 && v.NT > kThreads) continue;
+    if (tile_env) {
+      int th = 0, tw = 0;
+      if (sscanf(tile_env, "%dx%d", &th, &tw) == 2 && (th != v.TH || tw != v.TW)) continue;
+    }
     if (d->H % v.TH || d->W % v.TW || ry > v.RY || rx > v.RX) continue;
     if (v.KU > 0 ? !(P->graph_on && !zp && !P->need_k0 && P->k == v.KU) : P->graph_on) continue;
     const K1Layout L = k1_layout(CP, HDP, v.TH, v.TW, v.RY, v.RX, P->k);
