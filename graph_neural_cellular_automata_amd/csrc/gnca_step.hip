@@ -1121,10 +1121,12 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->tiles_y = (d->H + bth - 1) / bth;
   P->tps = P->tiles_x * P->tiles_y;
   P->total_tiles = P->tps * d->B;
-  // K2 bands: ~8 row bands per sample (many small workgroups: no wave-quantisation tail),
+  // K2 bands: ~6 row bands per sample (many small workgroups: no wave-quantisation tail),
   // each with its alpha rows + 2 halo rows and its post mask in LDS (<= 48 KB)
   {
-    long rows = (d->H + 7) / 8;
+    long rows = (d->H + 5) / 6;
+    static const char* band_env = getenv("GNCA_K2_BAND");   // measurement knob (A/B runs only)
+    if (band_env && atoi(band_env) > 0) rows = atoi(band_env);
     const long cap = (48L * 1024 / 4 / d->W - 2) / 2;
     if (rows > cap) rows = cap;
     if (rows < 1) rows = 1;
