@@ -60,7 +60,7 @@ class Grads(ctypes.Structure):
 EXPORTS = ("gnca_abi_version", "gnca_status_string", "gnca_last_hip_error",
            "gnca_workspace_bytes", "gnca_step_f32", "gnca_step_phases_f32", "gnca_message_f32",
            "gnca_perceive_f32", "gnca_rollout_f32", "gnca_bwd_workspace_bytes", "gnca_step_bwd_f32",
-           "gnca_fire_mask_u8")
+           "gnca_fire_mask_u8", "gnca_step_masked_f32")
 
 PHASE_K0, PHASE_K1, PHASE_K2 = 1, 2, 4
 PHASE_ALL = 7
@@ -109,7 +109,10 @@ def load(path: str = LIB_PATH):
     lib.gnca_bwd_workspace_bytes.argtypes = [ctypes.POINTER(StepDesc)]
     lib.gnca_step_bwd_f32.restype = ctypes.c_int
     lib.gnca_step_bwd_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights), vp, vp, vp,
-                                      vp, ctypes.POINTER(Grads), vp, vp, sz, vp]
+                                      vp, vp, ctypes.POINTER(Grads), vp, vp, sz, vp]
+    lib.gnca_step_masked_f32.restype = ctypes.c_int
+    lib.gnca_step_masked_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights), vp, vp, vp,
+                                         vp, vp, sz, vp]
     v = lib.gnca_abi_version()
     if v != ABI_VERSION:
         raise GncaError(f"libgnca.so ABI version {v} != expected {ABI_VERSION}; rebuild it")

@@ -102,6 +102,7 @@ struct BAArgs {
   float* gx;
   float* U;
   double* part;   // [B * nbands][2 + 2C]: sum U, sum U*xhat, then (sum g_xn*xhat, sum g_xn) per c
+  const uint8_t* active;   // masked step: inactive samples pass the gradient through
   int B, C, H, W, tps, band, nbands;
   float gain, thr, eps;
   int use_gn;
@@ -118,6 +119,17 @@ __global__ __launch_bounds__(kThreads) void gnca_b_gnprep(const BAArgs a) {
   const int h0 = max(0, r0 - 1), h1 = min(H, r1 + 1);
   const size_t HW = (size_t)H * W;
   const bool gn = a.use_gn != 0;
+  if (a.active && !a.active[b]) {   // x_out = x for this sample: gx = gy, nothing else
+    const int nbc = (r1 - r0) * W;
+    for (int it = tid; it < C * nbc; it += kThreads) {
+      const int c = it / nbc, e = it - c * nbc;
+      const size_t p = (size_t)b * C * HW + (size_t)c * HW + (size_t)r0 * W + e;
+      a.gx[p] = a.gy[p];
+      a.U[p] = 0.f;
+    }
+    if (tid < 2 + 2 * C) a.part[(size_t)blockIdx.x * (2 + 2 * C) + tid] = 0.0;
+    return;
+  }
   if (tid == 0) {
     float mu = 0.f, rs = 1.f;
     if (gn) sample_stats(a.stats, b, a.tps, (double)C * (double)HW, a.eps, &mu, &rs);
@@ -276,6 +288,7 @@ struct BBArgs {
   const float* wm;
   const float* bm;
   const float* offw;   // [B*k] zero-pad weights or null (uniform 1/k)
+  const uint8_t* active;   // masked step: inactive samples have no update (all cells dead)
   float* dY;           // [B, 3C, H, W]
   float* dG;           // [B, C, H, W]
   float* dmb;          // [B, H, W] <dm, b_M> (zero-pad only) or null
@@ -420,6 +433,19 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     float* dYb = a.dY + (size_t)b * 3 * C * HW;
     float* dGb = a.dG + (size_t)b * C * HW;
     __syncthreads();
+    if (a.active && !a.active[b]) {   // masked step, inactive sample: every cell is dead
+      if (first)
+        for (int n = tid; n < ncell; n += kThreads) {
+          const int ti = n / TW, tj = n - (n / TW) * TW;
+          if (i0 + ti >= H || j0 + tj >= W) continue;
+          const int ce = (i0 + ti) * W + (j0 + tj);
+          for (int pl = 0; pl < 3 * C; ++pl) dYb[pl * HWi + ce] = 0.f;
+          if (msg)
+            for (int c = 0; c < C; ++c) dGb[c * HWi + ce] = 0.f;
+          if (a.dmb) a.dmb[(size_t)b * HW + ce] = 0.f;
+        }
+      continue;
+    }
     // ---- staging by LDS-DMA (as the forward K1): every channel plane of the (RH x RW) region
     //      and the alpha plane with one more ring, all loads in flight at once, no VGPR round
     //      trip; torus-wrapped, or a zero source outside the image in pad mode ----
@@ -874,6 +900,7 @@ struct BCArgs {
   const float* x;
   const float* perc;
   const float* offw;
+  const uint8_t* active;
   float* gx;
   int B, C, H, W, k, TH, TW, tiles_x, tps, RY, RX;
   float graph_alpha_thr, uniform_w;
@@ -894,6 +921,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int b = blockIdx.x / a.tps, tin = blockIdx.x - b * a.tps;
+  if (a.active && !a.active[b]) return;   // dY = dG = 0 for an inactive sample
   const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
   const int RY = a.RY, RX = a.RX, H = a.H, W = a.W, C = a.C, k = a.k;
   const int TH = a.TH, TW = a.TW, PW = TW + 2, PA = (TH + 2) * PW;
@@ -1473,8 +1501,9 @@ size_t gnca_bwd_workspace_bytes(const gnca_step_desc* desc) {
 }
 
 int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
-                      const void* fire, const float* gy, float* gx, const gnca_grads* grads,
-                      const void* saved, void* ws, size_t ws_bytes, void* stream) {
+                      const void* fire, const uint8_t* active, const float* gy, float* gx,
+                      const gnca_grads* grads, const void* saved, void* ws, size_t ws_bytes,
+                      void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (!desc || !w || !x || !gy || !gx || !grads) return GNCA_ERR_INVALID;
   if (gx == x || gx == gy) return GNCA_ERR_INVALID;
@@ -1493,9 +1522,14 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
   // F: recompute the forward's dx / GroupNorm partials / offset weights (gx is a dummy x_out:
   // phase K2, the only writer of x_out, is not run)
   const char* fw = saved ? reinterpret_cast<const char*>(saved) : wsb + P.off_fwd;
-  if (!saved && (rc = gnca_step_phases_f32(&d, w, x, gx, fire, nullptr, wsb + P.off_fwd, P.F.ws_bytes,
-                                           stream, GNCA_PHASE_K0 | GNCA_PHASE_K1)) != GNCA_OK)
-    return rc;
+  if (!saved) {
+    // recompute dx / partials / offset weights (K2, the only writer of x_out = gx here, is not run)
+    rc = active ? gnca_step_masked_phases(&d, w, x, gx, fire, active, wsb + P.off_fwd, P.F.ws_bytes,
+                                          stream, GNCA_PHASE_K0 | GNCA_PHASE_K1)
+                : gnca_step_phases_f32(&d, w, x, gx, fire, nullptr, wsb + P.off_fwd, P.F.ws_bytes, stream,
+                                       GNCA_PHASE_K0 | GNCA_PHASE_K1);
+    if (rc != GNCA_OK) return rc;
+  }
   const float* dx = reinterpret_cast<const float*>(fw + P.F.off_dx);
   const double* stats = reinterpret_cast<const double*>(fw + P.F.off_stats);
   const float* offw = (P.msg && P.zp) ? reinterpret_cast<const float*>(fw + P.F.off_offw) : nullptr;
@@ -1511,7 +1545,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     BAArgs a;
     memset(&a, 0, sizeof(a));
     a.x = x; a.dx = dx; a.gy = gy; a.gamma = w->gn_weight; a.beta = w->gn_bias; a.stats = stats;
-    a.gx = gx; a.U = U; a.part = pa;
+    a.gx = gx; a.U = U; a.part = pa; a.active = active;
     a.B = B; a.C = C; a.H = H; a.W = W; a.tps = P.F.tps; a.band = P.band; a.nbands = P.nbands;
     a.gain = d.update_gain; a.thr = d.alpha_thr; a.eps = d.gn_eps; a.use_gn = P.gn ? 1 : 0;
     hipLaunchKernelGGL(gnca_b_gnprep, dim3(B * P.nbands), dim3(kThreads), P.ldsA, st, a);
@@ -1527,7 +1561,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     memset(&a, 0, sizeof(a));
     a.x = x; a.U = U; a.dx = dx; a.coef = coef; a.fire = fire;
     a.perc = w->perception; a.w1 = w->w1; a.b1 = w->b1; a.w2 = w->w2; a.wm = w->wm; a.bm = w->bm;
-    a.offw = offw; a.dY = dY; a.dG = dG; a.dmb = dmb; a.part = pb;
+    a.offw = offw; a.active = active; a.dY = dY; a.dG = dG; a.dmb = dmb; a.part = pb;
     a.seed = d.rng_seed; a.rng_step = d.rng_step; a.sample_base = d.sample_base;
     a.B = B; a.C = C; a.H = H; a.W = W; a.hidden = Hd; a.k = P.msg ? P.F.k : 0;
     a.RY = P.RY; a.RX = P.RX; a.TH = P.TH; a.TW = P.TW; a.tiles_x = P.tiles_x; a.tps = P.tps;
@@ -1556,6 +1590,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     BCArgs a;
     memset(&a, 0, sizeof(a));
     a.dY = dY; a.dG = dG; a.x = x; a.perc = w->perception; a.offw = offw; a.gx = gx;
+    a.active = active;
     a.B = B; a.C = C; a.H = H; a.W = W; a.k = P.msg ? P.F.k : 0;
     a.TH = P.TH3; a.TW = P.TW3; a.tiles_x = P.tiles_x3; a.tps = P.tps3;
     a.RY = P.RY; a.RX = P.zp ? 0 : P.RX;

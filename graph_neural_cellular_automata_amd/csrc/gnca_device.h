@@ -60,6 +60,11 @@ struct FwdLayout {
 };
 bool fwd_layout(const gnca_step_desc* d, FwdLayout* out);
 
+// gnca_step_phases_f32 restricted to active samples (the masked step; used by the backward)
+int gnca_step_masked_phases(const gnca_step_desc* d, const gnca_weights* w, const float* x, float* x_out,
+                            const void* fire, const uint8_t* active, void* ws, size_t ws_bytes,
+                            void* stream, uint32_t phases);
+
 // hipError_t of the last failed launch on this thread (gnca_last_hip_error)
 extern thread_local int g_last_hip;
 

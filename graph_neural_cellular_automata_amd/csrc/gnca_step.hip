@@ -115,6 +115,7 @@ struct K1Args {
   const float* bm;
   const float* offw;   // [B * k] per-sample offset weights, or null -> uniform_w
   const void* fire;
+  const uint8_t* active;   // [B] or null: samples with active[b] == 0 are skipped (K2 copies them)
   uint64_t seed;
   int64_t rng_step;
   int64_t sample_base;
@@ -285,6 +286,13 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
     const float* xb = a.x + (size_t)b * C * HW;
+    if (a.active && !a.active[b]) {   // inactive sample (masked step): nothing to update
+      if (tid == 0 && !msg_only) {
+        a.stats[(size_t)tile * 2 + 0] = 0.0;
+        a.stats[(size_t)tile * 2 + 1] = 0.0;
+      }
+      continue;
+    }
     __syncthreads();  // previous tile's LDS readers are done (and the fragment staging area)
 
     // ---- LDS-DMA staging: the (RH x RW) region of every channel, then the alpha plane with one
@@ -713,6 +721,7 @@ struct K2Args {
   int B, C, H, W, tps, band, nbands;
   float gain, thr, eps;
   int use_gn;
+  const uint8_t* active;   // [B] or null: inactive samples are copied through unchanged
 };
 
 // One workgroup per (sample, band of rows).  LDS: the updated alpha x~_3 over the band + one
@@ -727,6 +736,16 @@ __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
   const int r0 = band * a.band, r1 = min(H, r0 + a.band);
   const int h0 = max(0, r0 - 1), h1 = min(H, r1 + 1);       // alpha rows incl. halo
   const size_t HW = (size_t)H * W;
+  if (a.active && !a.active[b]) {   // masked step: an inactive sample passes through unchanged
+    const float* xs_ = a.x + (size_t)b * C * HW;
+    float* os_ = a.out + (size_t)b * C * HW;
+    const int nbc = (r1 - r0) * W;
+    for (int it = tid; it < C * nbc; it += kThreads) {
+      const int c = it / nbc, e = it - c * nbc;
+      os_[(size_t)c * HW + (size_t)r0 * W + e] = xs_[(size_t)c * HW + (size_t)r0 * W + e];
+    }
+    return;
+  }
 
   if (tid == 0) {
     float mu = 0.f, rs = 1.f;
@@ -1152,6 +1171,10 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   return true;
 }
 
+int gnca_step_masked_phases(const gnca_step_desc* d, const gnca_weights* w, const float* x, float* x_out,
+                            const void* fire, const uint8_t* active, void* ws, size_t ws_bytes,
+                            void* stream, uint32_t phases);
+
 bool fwd_layout(const gnca_step_desc* d, FwdLayout* out) {
   Plan P;
   if (!make_plan(d, false, &P)) return false;
@@ -1287,7 +1310,7 @@ static bool weights_ok(const gnca_step_desc* d, const gnca_weights* w, bool msg_
 
 static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float* x, float* x_out,
                      const void* fire, float* attn, void* ws, size_t ws_bytes, hipStream_t st,
-                     uint32_t phases = GNCA_PHASE_ALL) {
+                     uint32_t phases = GNCA_PHASE_ALL, const uint8_t* active = nullptr) {
   Plan P;
   if (!make_plan(d, false, &P)) {
     if (d && d->C >= 4 && d->hidden > 0 && !find_variant(d->C, d->hidden)) return GNCA_ERR_UNSUPPORTED;
@@ -1312,6 +1335,7 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   K1Args k1;
   float* dx = reinterpret_cast<float*>(wsb + P.off_dx);
   fill_k1(k1, d, w, P, x, dx, fire, want_attn ? attn : nullptr, wsb);
+  k1.active = active;
   if ((phases & GNCA_PHASE_K1) && (rc = launch_k1(k1, P, st)) != GNCA_OK) return rc;
   if (!(phases & GNCA_PHASE_K2)) return GNCA_OK;
   K2Args k2;
@@ -1325,8 +1349,16 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   k2.B = d->B; k2.C = d->C; k2.H = d->H; k2.W = d->W; k2.tps = P.tps;
   k2.band = P.band; k2.nbands = P.nbands;
   k2.gain = d->update_gain; k2.thr = d->alpha_thr; k2.eps = d->gn_eps;
+  k2.active = active;
   hipLaunchKernelGGL(gnca_k2_finalize, dim3(P.total2), dim3(kThreads), P.lds2, st, k2);
   return check_launch();
+}
+
+int gnca_step_masked_phases(const gnca_step_desc* d, const gnca_weights* w, const float* x, float* x_out,
+                            const void* fire, const uint8_t* active, void* ws, size_t ws_bytes,
+                            void* stream, uint32_t phases) {
+  return step_impl(d, w, x, x_out, fire, nullptr, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream),
+                   phases, active);
 }
 
 }  // namespace gnca
@@ -1362,6 +1394,14 @@ size_t gnca_workspace_bytes(const gnca_step_desc* desc) {
 int gnca_step_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x, float* x_out,
                   const void* fire, float* attn, void* ws, size_t ws_bytes, void* stream) {
   return step_impl(desc, w, x, x_out, fire, attn, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream));
+}
+
+int gnca_step_masked_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
+                         float* x_out, const void* fire, const uint8_t* active, void* ws,
+                         size_t ws_bytes, void* stream) {
+  if (!active || (desc && (desc->flags & GNCA_ATTENTION))) return GNCA_ERR_INVALID;
+  return step_impl(desc, w, x, x_out, fire, nullptr, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream),
+                   GNCA_PHASE_ALL, active);
 }
 
 int gnca_step_phases_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,

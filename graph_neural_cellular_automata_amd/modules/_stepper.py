@@ -21,14 +21,15 @@ class _StepFn(torch.autograd.Function):
     drawn (``graph_augmentation.py:141-147`` returns zeros without touching them)."""
 
     @staticmethod
-    def forward(ctx, x, desc, weights, keep, fire, want_attn, names, *params):
+    def forward(ctx, x, desc, weights, keep, fire, want_attn, names, active, *params):
         ws = S.workspace(desc, x.device)   # kept: the backward reuses its update field
-        out, attn = S.step(desc, weights, x, fire=fire, want_attention=want_attn, ws=ws)
+        out, attn = S.step(desc, weights, x, fire=fire, want_attention=want_attn, ws=ws, active=active)
         if attn is not None:
             ctx.mark_non_differentiable(attn)
         ctx.save_for_backward(x)
         ctx.desc, ctx.weights, ctx.keep, ctx.fire, ctx.names = desc, weights, keep, fire, names
         ctx.ws = ws
+        ctx.active = active
         ctx.params = params
         return out, attn
 
@@ -37,7 +38,7 @@ class _StepFn(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         desc = ctx.desc
         no_graph_use = (desc.flags & L.GRAPH) and desc.num_offsets == 0
-        need = ctx.needs_input_grad[7:]
+        need = ctx.needs_input_grad[8:]
         want = {}
         for name, p, nd in zip(ctx.names, ctx.params, need):
             if not nd or name not in S.GRAD_FIELDS:
@@ -46,14 +47,15 @@ class _StepFn(torch.autograd.Function):
                 continue
             want[name] = p
         gx, grads = S.step_backward(desc, ctx.weights, x, gout.contiguous(), fire=ctx.fire, want=want,
-                                    saved=ctx.ws)
+                                    saved=ctx.ws, active=ctx.active)
         ctx.ws = None
         pgrads = [grads.get(n) for n in ctx.names]
-        return (gx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, *pgrads)
+        return (gx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, None,
+                *pgrads)
 
 
 def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen, message_gain,
-             hidden_only: bool, return_attention: bool):
+             hidden_only: bool, return_attention: bool, active=None):
     x = S.check_state(x, model.n_channels)
     B, C, H, W = x.shape
     flags = 0
@@ -95,7 +97,7 @@ def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen,
     if torch.is_grad_enabled() and (x.requires_grad or named):
         names = tuple(n for n, _ in named)
         params = [p for _, p in named]
-        out, attn = _StepFn.apply(x, desc, w, keep, fire, return_attention, names, *params)
+        out, attn = _StepFn.apply(x, desc, w, keep, fire, return_attention, names, active, *params)
     else:
-        out, attn = S.step(desc, w, x, fire=fire, want_attention=return_attention)
+        out, attn = S.step(desc, w, x, fire=fire, want_attention=return_attention, active=active)
     return out, attn

@@ -30,7 +30,8 @@ class NeuralCA(nn.Module):
         """max_pool2d(alpha, 3, 1, 1) > alpha_thr (nca.py:55-62); a helper, not the step."""
         return (F.max_pool2d(x[:, 3:4], kernel_size=3, stride=1, padding=1) > self.alpha_thr).float()
 
-    def forward(self, x: torch.Tensor, fire_rate: float = 1.0) -> torch.Tensor:
-        """One CA step on the HIP path (nca.py:64-105)."""
-        out, _ = run_step(self, x, fire_rate, None, None, 0.0, False, False)
+    def forward(self, x: torch.Tensor, fire_rate: float = 1.0, *,
+                active: torch.Tensor | None = None) -> torch.Tensor:
+        """One CA step on the HIP path (nca.py:64-105).  ``active``: see NeuralCAGraph.forward."""
+        out, _ = run_step(self, x, fire_rate, None, None, 0.0, False, False, active=active)
         return out

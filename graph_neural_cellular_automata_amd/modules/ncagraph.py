@@ -57,9 +57,15 @@ class NeuralCAGraph(nn.Module):
             m = torch.cat([torch.zeros_like(m[:, :4]), m[:, 4:]], dim=1)
         return torch.tanh(m) * self.message_gain
 
-    def forward(self, x: torch.Tensor, fire_rate: float = 1.0, *, return_attention: bool = False):
-        """One CA step with the mid-range graph message, on the HIP path (ncagraph.py:106-168)."""
+    def forward(self, x: torch.Tensor, fire_rate: float = 1.0, *, return_attention: bool = False,
+                active: torch.Tensor | None = None):
+        """One CA step with the mid-range graph message, on the HIP path (ncagraph.py:106-168).
+
+        ``active`` (extension, not in the reference): a [B] bool mask; ``model(x, fr, active=m)``
+        equals the trainers' ``x[m] = model(x[m], fr)`` (train_graph_augmented_nca.py:305-321)
+        without the sub-batch gather/scatter, except that the fire uniforms are drawn for the
+        whole batch (``torch.rand(B,1,H,W)``) rather than for the active rows only."""
         chosen = self.graph.sample_offsets()
         out, attn = run_step(self, x, fire_rate, self.graph, chosen, self.message_gain,
-                             self.hidden_only, return_attention)
+                             self.hidden_only, return_attention, active=active)
         return (out, attn) if return_attention else out

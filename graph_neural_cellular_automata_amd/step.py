@@ -90,15 +90,34 @@ def stream_ptr(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-def step(desc, weights, x, fire=None, want_attention=False, ws=None):
+def _active_u8(active, B, device):
+    if active is None:
+        return None
+    if active.device != device or active.dtype not in (torch.bool, torch.uint8) or active.shape != (B,):
+        raise ValueError("active must be a [B] bool/uint8 tensor on the state's device")
+    return active.to(torch.uint8).contiguous()
+
+
+def step(desc, weights, x, fire=None, want_attention=False, ws=None, active=None):
     """One step: returns (x_out, attn_or_None).  ``ws``: an optional caller-owned workspace
-    (``workspace(desc)``); after the call it holds what ``step_backward(saved=ws)`` reuses."""
+    (``workspace(desc)``); after the call it holds what ``step_backward(saved=ws)`` reuses.
+    ``active``: optional [B] bool/uint8 device mask; inactive samples pass through unchanged
+    (gnca_step_masked_f32)."""
     lib = L.load()
     x_out = torch.empty_like(x)
     attn = torch.empty(desc.B, desc.H, desc.W, dtype=torch.float32, device=x.device) \
         if want_attention else None
     if ws is None:
         ws = workspace(desc, x.device)
+    act = _active_u8(active, desc.B, x.device)
+    if act is not None:
+        if want_attention:
+            raise ValueError("return_attention is not supported with an active-sample mask")
+        rc = lib.gnca_step_masked_f32(ctypes.byref(desc), ctypes.byref(weights), x.data_ptr(),
+                                      x_out.data_ptr(), _ptr(fire), act.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), stream_ptr(x.device))
+        L.check(rc, "gnca_step_masked_f32")
+        return x_out, None
     rc = lib.gnca_step_f32(ctypes.byref(desc), ctypes.byref(weights), x.data_ptr(),
                            x_out.data_ptr(), _ptr(fire), _ptr(attn), ws.data_ptr(), ws.numel(),
                            stream_ptr(x.device))
@@ -166,7 +185,7 @@ GRAD_FIELDS = {
 }
 
 
-def step_backward(desc, weights, x, gy, fire=None, want: dict | None = None, saved=None):
+def step_backward(desc, weights, x, gy, fire=None, want: dict | None = None, saved=None, active=None):
     """Vector-Jacobian product of one step (gnca_step_bwd_f32).
 
     ``want`` maps state_dict names (GRAD_FIELDS keys) to the parameter tensors whose gradients
@@ -188,8 +207,9 @@ def step_backward(desc, weights, x, gy, fire=None, want: dict | None = None, sav
             f"unsupported step shape for the backward: B={desc.B} C={desc.C} H={desc.H} "
             f"W={desc.W} hidden={desc.hidden}")
     ws = torch.empty(n, dtype=torch.uint8, device=x.device)
+    act = _active_u8(active, desc.B, x.device)
     rc = lib.gnca_step_bwd_f32(ctypes.byref(desc), ctypes.byref(weights), x.data_ptr(), _ptr(fire),
-                               gy.data_ptr(), gx.data_ptr(), ctypes.byref(g), _ptr(saved),
+                               _ptr(act), gy.data_ptr(), gx.data_ptr(), ctypes.byref(g), _ptr(saved),
                                ws.data_ptr(), ws.numel(), stream_ptr(x.device))
     L.check(rc, "gnca_step_bwd_f32")
     return gx, out

@@ -124,6 +124,18 @@ int gnca_step_f32(const gnca_step_desc* desc, const gnca_weights* w, const float
                   float* x_out, const void* fire, float* attn, void* ws, size_t ws_bytes,
                   void* stream);
 
+/*
+ * One step restricted to the samples with active[b] != 0 (active: uint8 [B], device memory); the
+ * other samples are copied through unchanged and do not fire.  Replaces the trainers'
+ * `state[mask] = model(state[mask], fire_rate)` variable-length rollout masking
+ * (src/training/train_graph_augmented_nca.py:305-321) without the gather/scatter copies of the
+ * sub-batch and without a host-side mask.any() sync.  `fire` (GNCA_FIRE_RAND_F32 / MASK_U8) is
+ * indexed by the full batch; GNCA_ATTENTION is not supported here.
+ */
+int gnca_step_masked_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
+                         float* x_out, const void* fire, const uint8_t* active, void* ws,
+                         size_t ws_bytes, void* stream);
+
 /* Measurement hook: run only the step's kernels named in `phases` (GNCA_PHASE_* bits) with the
  * same arguments as gnca_step_f32.  gnca_step_f32 == all phases.  Skipping a phase leaves its
  * outputs stale; bench.py uses this to time K1 alone with HIP events on `stream`. */
@@ -192,13 +204,16 @@ size_t gnca_bwd_workspace_bytes(const gnca_step_desc* desc);
  * gradients.  The alive / fire masks are constants, the perception weight is frozen (no
  * gradient), as in the reference's autograd graph.  In torus mode the offset weights are exactly
  * uniform, so the query/key/scaling gradients are exactly zero.  gx must not alias x or gy.
+ *   active: NULL, or the uint8 [B] sample mask of a gnca_step_masked_f32 forward (inactive
+ *           samples: gx = gy, no parameter gradient).
  *   saved: the workspace of the gnca_step_f32 call that produced x_out (same desc, weights, x
  *          and fire), kept unmodified since: its update field and GroupNorm partials are reused.
  *          NULL: the backward recomputes them (one more forward pass).
  */
 int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
-                      const void* fire, const float* gy, float* gx, const gnca_grads* grads,
-                      const void* saved, void* ws, size_t ws_bytes, void* stream);
+                      const void* fire, const uint8_t* active, const float* gy, float* gx,
+                      const gnca_grads* grads, const void* saved, void* ws, size_t ws_bytes,
+                      void* stream);
 
 #ifdef __cplusplus
 }

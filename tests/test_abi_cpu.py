@@ -120,6 +120,8 @@ def test_bwd_rejects_bad_args_without_touching_gpu(lib):
     d = _desc()
     w = L.Weights()
     g = L.Grads()
-    rc = lib.gnca_step_bwd_f32(ctypes.byref(d), ctypes.byref(w), None, None, None, None, ctypes.byref(g),
-                               None, None, 0, None)
+    rc = lib.gnca_step_bwd_f32(ctypes.byref(d), ctypes.byref(w), None, None, None, None, None,
+                               ctypes.byref(g), None, None, 0, None)
+    rc2 = lib.gnca_step_masked_f32(ctypes.byref(d), ctypes.byref(w), None, None, None, None, None, 0, None)
+    assert rc2 == -1
     assert rc == -1
