@@ -69,7 +69,6 @@ def parse():
                          "trainer's BPTT iteration (SURVEY.md §8f rank 1), steps = iterations")
     ap.add_argument("--train-batch", type=int, default=16, help="train: samples per GPU (config.json)")
     ap.add_argument("--train-size", type=int, default=40, help="train: canvas (config.json img_size)")
-    ap.add_argument("--train-rollout", type=int, default=64, help="train: CA steps per iteration")
     return ap.parse_args()
 
 
@@ -147,36 +146,50 @@ def cpu_baseline(budget_s: float):
 
 
 def main_train(args, dev, world, rank):
-    """One data-parallel BPTT iteration of the graph trainer (train_graph_augmented_nca.py:289-375):
-    rollout (fire rate ~ U(0.5, 0.9) per step, message every 3rd step), premultiplied-RGBA MSE,
-    loss.backward() through the HIP step, one flat RCCL gradient all-reduce, per-parameter grad
-    normalisation, Adam.  Weak scaling: ``--train-batch`` samples per GPU."""
+    """One data-parallel iteration of the graph trainer (train_graph_augmented_nca.py:289-391), on
+    the package's device-side pieces: sample a batch from the device-resident pool (this rank's
+    shard of the 1024-slot pool), per-sample rollout lengths (48-80 steps), masked steps
+    (``active = nca_steps > t``: no sub-batch gather/scatter, no per-step host sync), fire rate
+    ~ U(0.5, 0.9) and the message on every 3rd step, premultiplied-RGBA MSE, loss.backward()
+    through the HIP step, one flat RCCL gradient all-reduce, per-parameter grad normalisation,
+    Adam, pool replace.  Weak scaling: ``--train-batch`` samples per GPU."""
     import torch.distributed as dist
     from graph_neural_cellular_automata_amd import NeuralCAGraph
     from graph_neural_cellular_automata_amd.dp import allreduce_gradients, normalize_gradients_
-    torch.manual_seed(7 + rank)
+    from graph_neural_cellular_automata_amd.pool import SamplePool
+    torch.manual_seed(7)
     random.seed(42)                       # identical offset draws / fire rates on every rank
     model = NeuralCAGraph(C, HD, update_gain=GAIN, alpha_thr=THR, message_gain=MSG_GAIN,
                           graph_d_model=D_MODEL, graph_attention_radius=R, graph_num_neighbors=K,
                           graph_zero_padded_shift=False).to(dev)
-    sd = {k: v for k, v in load_weights(dev).items()}
-    model.load_state_dict(sd, strict=False)
+    model.load_state_dict({k: v for k, v in load_weights(dev).items()}, strict=False)
     opt = torch.optim.Adam(model.parameters(), lr=2e-4, weight_decay=1e-5)
     params = [p for p in model.parameters() if p.requires_grad]
-    B, H, T = args.train_batch, args.train_size, args.train_rollout
-    g = torch.Generator(device=dev).manual_seed(99 + rank)
-    x0 = torch.rand(B, C, H, H, device=dev, generator=g)
-    x0[:, 4:] = torch.randn(B, C - 4, H, H, device=dev, generator=g)
-    target = torch.rand(4, H, H, device=dev, generator=g)
+    B, H = args.train_batch, args.train_size
+    lo_steps, hi_steps = 48, 80
+
+    def seed_fn(batch_size=1):            # train_graph_augmented_nca.py:108-114
+        g = torch.zeros(batch_size, C, H, H, device=dev)
+        g[:, 3:4, H // 2, H // 2] = 1.0
+        g[:, 4:, H // 2, H // 2] = 0.01 * torch.randn_like(g[:, 4:, H // 2, H // 2])
+        return g
+
+    pool = SamplePool(1024 * world, seed_fn, device=dev, shard=(rank, world))
+    gen = torch.Generator(device=dev).manual_seed(99 + rank)
+    target = torch.rand(4, H, H, device=dev, generator=gen)
     target[:3] *= target[3:4]
+    cells = [0]
 
     def iteration():
-        state = x0.clone()
+        idx, state = pool.sample(B)
+        nsteps = torch.randint(lo_steps, hi_steps + 1, (B,), device=dev, generator=gen)
+        T = int(nsteps.max().item())
         for t in range(T):
             fr = random.uniform(0.5, 0.9)
             model.message_gain = MSG_GAIN if t % 3 == 0 else 0.0   # message_every = 3
-            state = model(state, fire_rate=fr)
+            state = model(state, fire_rate=fr, active=nsteps > t)
         model.message_gain = MSG_GAIN
+        cells[0] += int(nsteps.sum().item()) * H * H
         rgba = torch.cat([state[:, :3] * state[:, 3:4], state[:, 3:4]], 1)
         loss = ((rgba - target[None]) ** 2).mean()
         opt.zero_grad(set_to_none=True)
@@ -184,6 +197,7 @@ def main_train(args, dev, world, rank):
         allreduce_gradients(params)
         normalize_gradients_(params)
         opt.step()
+        pool.replace(idx, state)
         return loss
 
     for _ in range(args.warmup):
@@ -192,6 +206,7 @@ def main_train(args, dev, world, rank):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    cells[0] = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = iteration()
@@ -199,24 +214,27 @@ def main_train(args, dev, world, rank):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    tot = torch.tensor([float(cells[0])], dtype=torch.float64,
+                       device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+        dist.all_reduce(tot)
     if rank == 0:
-        cells = B * H * H * T * args.steps * world
         line = {
             "metric": "BPTT training cell-updates/sec (forward+backward through the CA step), "
                       "graph trainer iteration",
-            "value": cells / el, "unit": "cell-updates/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic states and target; trained nca_latest.pt weights (golden fixture)",
-            "config": {"workload": f"graph trainer BPTT iteration: rollout {T} steps, fire U(0.5,0.9), "
-                                   f"message every 3rd step, premult-RGBA MSE, RCCL flat grad "
-                                   f"all-reduce, grad/||grad||, Adam", "channels": C, "hidden": HD,
-                       "height": H, "width": H, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"dp{world}"},
+            "value": float(tot.item()) / el, "unit": "cell-updates/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic target; trainer seed states; trained nca_latest.pt weights (golden fixture)",
+            "config": {"workload": f"graph trainer iteration: device pool (1024/GPU), per-sample "
+                                   f"rollouts {lo_steps}-{hi_steps} steps via the masked step, fire "
+                                   f"U(0.5,0.9), message every 3rd step, premult-RGBA MSE, RCCL flat "
+                                   f"grad all-reduce, grad/||grad||, Adam, pool replace",
+                       "channels": C, "hidden": HD, "height": H, "width": H, "batch_per_gpu": B,
+                       "global_batch": B * world, "parallelism": f"dp{world}"},
             "iterations_per_s": args.steps / el, "final_loss": float(loss.detach()),
         }
         print(json.dumps(line), flush=True)

@@ -1,0 +1,55 @@
+"""Device-resident sample pool, the caller-side data format of the path.
+
+Mirror of the reference's ``SamplePool`` (``src/training/pool.py:5-42``) with the same
+constructor, ``sample`` and ``replace`` (same argument meaning and the same Python ``random``
+consumption), but the pool is ONE contiguous ``[P, C, H, W]`` device tensor instead of a list of
+P separate tensors: ``sample`` is one ``index_select`` (the reference stacks B clones) and
+``replace`` one ``index_copy_`` (the reference assigns B clones one by one).  On a 288 GB MI355X the
+whole C4 pool (1024 x 16 x 72 x 72 fp32 = 340 MB) stays resident.
+
+Multi-GPU (``shard=(rank, world)``): each rank keeps only its contiguous slice of the pool
+(``sharding.shard_range``) and samples its share of the batch from it.  Every rank still calls
+``seed_fn`` for all P samples, so the global RNG streams stay identical across ranks.
+"""
+from __future__ import annotations
+
+import random
+
+import torch
+
+from .sharding import shard_range
+
+
+class SamplePool:
+    def __init__(self, pool_size, seed_fn, device="cpu", *, shard: tuple[int, int] | None = None):
+        """``seed_fn(batch_size=1)`` returns one seed state ([1,C,H,W] or [C,H,W]), called once per
+        pool slot exactly as the reference does (pool.py:18)."""
+        self.pool_size = int(pool_size)
+        rank, world = shard if shard is not None else (0, 1)
+        self.lo, self.hi = shard_range(self.pool_size, rank, world)
+        seeds = []
+        for i in range(self.pool_size):
+            s = seed_fn(batch_size=1)
+            if i >= self.lo and i < self.hi:
+                seeds.append(s.reshape(s.shape[-3:]).to(device))
+        self.states = torch.stack(seeds).contiguous() if seeds else torch.empty(0, device=device)
+
+    def __len__(self):
+        return self.states.shape[0]
+
+    @property
+    def pool(self):
+        """The slots as a list of [C,H,W] views (the reference's attribute, for reading)."""
+        return list(self.states.unbind(0))
+
+    def sample(self, batch_size):
+        """(idx, batch): ``random.sample`` over this pool's slots (pool.py:23-32) and a fresh
+        [B,C,H,W] tensor (a copy: the pool is not modified through it)."""
+        idx = random.sample(range(len(self)), batch_size)
+        sel = torch.as_tensor(idx, dtype=torch.long, device=self.states.device)
+        return idx, self.states.index_select(0, sel)
+
+    def replace(self, idx, new_samples):
+        """Write ``new_samples`` (detached) into slots ``idx`` (pool.py:34-42)."""
+        sel = torch.as_tensor(list(idx), dtype=torch.long, device=self.states.device)
+        self.states.index_copy_(0, sel, new_samples.detach().to(self.states.dtype))
