@@ -903,6 +903,7 @@ struct BCArgs {
   const uint8_t* active;
   float* gx;
   int B, C, H, W, k, TH, TW, tiles_x, tps, RY, RX;
+  int cpw, ncg;   // channels per workgroup, channel groups (small problems: more workgroups)
   float graph_alpha_thr, uniform_w;
   uint32_t flags;
   int8_t offs[2 * GNCA_MAX_OFFSETS];
@@ -920,8 +921,10 @@ __host__ __device__ inline int bc_stage(int TH, int TW, int RY, int RX, bool msg
 __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
-  const int b = blockIdx.x / a.tps, tin = blockIdx.x - b * a.tps;
+  const int cg = blockIdx.x % a.ncg, bt = blockIdx.x / a.ncg;
+  const int b = bt / a.tps, tin = bt - b * a.tps;
   if (a.active && !a.active[b]) return;   // dY = dG = 0 for an inactive sample
+  const int c_lo = cg * a.cpw, c_hi = min(a.C, c_lo + a.cpw);
   const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
   const int RY = a.RY, RX = a.RX, H = a.H, W = a.W, C = a.C, k = a.k;
   const int TH = a.TH, TW = a.TW, PW = TW + 2, PA = (TH + 2) * PW;
@@ -993,13 +996,13 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
     for (int i = 0; i < kBCStage; ++i)
       if (tid + kThreads * i < SE) dst[tid + kThreads * i] = stg[i];
   };
-  load(0);
+  load(c_lo);
   store(buf0);
   __syncthreads();
-  for (int c = 0; c < C; ++c) {
-    float* cur = (c & 1) ? buf1 : buf0;
-    float* nxt = (c & 1) ? buf0 : buf1;
-    if (c + 1 < C) load(c + 1);
+  for (int c = c_lo; c < c_hi; ++c) {
+    float* cur = ((c - c_lo) & 1) ? buf1 : buf0;
+    float* nxt = ((c - c_lo) & 1) ? buf0 : buf1;
+    if (c + 1 < c_hi) load(c + 1);
     const float* pw = pws + c * 27;
     for (int n = tid; n < TH * TW; n += kThreads) {
       const int ti = n / TW, tj = n % TW;
@@ -1027,7 +1030,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
       float* p = a.gx + ((size_t)b * C + c) * HW + (size_t)i * W + j;
       *p += acc;
     }
-    if (c + 1 < C) store(nxt);
+    if (c + 1 < c_hi) store(nxt);
     __syncthreads();
   }
 }
@@ -1239,8 +1242,9 @@ __global__ __launch_bounds__(kThreads) void gnca_b_rowcorr(float* gx, const floa
 }
 
 // R: fixed-order sums of partial rows into the gradient outputs (deterministic).
-// The output columns of up to 8 segments are numbered consecutively; segment s maps its local
-// column j to part column col0[s] + j*step[s] and writes out[s][j] (skipped if out[s] is null).
+// The output columns of up to 12 segments are numbered consecutively; segment s maps its local
+// column j to part column col0[s] + j*step[s] and writes out[s][j] (skipped if out[s] is null);
+// step[s] == 0 marks a segment of exact zeros (no reads).
 // A 256-thread block owns 16 columns: 16 row groups sum rows r = g, g+16, ... with 4 independent
 // accumulators each, then the 16 group sums are added in order.
 struct RedArgs {
@@ -1248,10 +1252,10 @@ struct RedArgs {
   int f64;
   long rows, stride;
   int nseg, ncols;
-  int end[8];       // exclusive end of segment s in the concatenated column space
-  long col0[8];
-  int step[8];
-  float* out[8];
+  int end[12];      // exclusive end of segment s in the concatenated column space
+  long col0[12];
+  int step[12];
+  float* out[12];
 };
 
 __global__ __launch_bounds__(kThreads) void gnca_b_reduce(const RedArgs a) {
@@ -1263,7 +1267,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_reduce(const RedArgs a) {
   const int begin = s == 0 ? 0 : a.end[s - 1];
   const long src = a.col0[s] + (long)(col - begin) * a.step[s];
   double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
-  if (col < a.ncols) {
+  if (col < a.ncols && a.step[s] != 0) {
     long r = rg;
     if (a.f64) {
       const double* p = reinterpret_cast<const double*>(a.part) + src;
@@ -1466,8 +1470,8 @@ struct Reducer {
     memset(&a, 0, sizeof(a));
     a.part = part; a.f64 = f64 ? 1 : 0; a.rows = rows; a.stride = stride;
   }
-  void add(long col0, int ncols, int step, float* out) {
-    if (ncols <= 0) return;
+  void add(long col0, int ncols, int step, float* out) {   // step 0: zeros
+    if (ncols <= 0 || !out) return;
     a.col0[a.nseg] = col0;
     a.step[a.nseg] = step;
     a.out[a.nseg] = out;
@@ -1482,10 +1486,6 @@ struct Reducer {
   }
 };
 
-static int zero_grad(float* p, size_t n, hipStream_t st) {
-  if (!p || n == 0) return GNCA_OK;
-  return hipMemsetAsync(p, 0, n * sizeof(float), st) == hipSuccess ? GNCA_OK : GNCA_ERR_HIP;
-}
 
 }  // namespace
 }  // namespace gnca
@@ -1593,14 +1593,20 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     a.active = active;
     a.B = B; a.C = C; a.H = H; a.W = W; a.k = P.msg ? P.F.k : 0;
     a.TH = P.TH3; a.TW = P.TW3; a.tiles_x = P.tiles_x3; a.tps = P.tps3;
+    // channel groups: enough workgroups to fill the chip when the batch is small
+    const long wgs = (long)B * P.tps3, want = 2L * bwd_device_cus();
+    a.ncg = (int)std::min<long>(C, std::max<long>(1, (want + wgs - 1) / wgs));
+    a.cpw = (C + a.ncg - 1) / a.ncg;
+    a.ncg = (C + a.cpw - 1) / a.cpw;
     a.RY = P.RY; a.RX = P.zp ? 0 : P.RX;
     a.graph_alpha_thr = d.graph_alpha_thr;
     a.uniform_w = P.F.k > 0 ? (float)(1.0 / (double)P.F.k) : 0.f;
     a.flags = (d.flags & (GNCA_ZERO_PAD_SHIFT | GNCA_ALIVE_TO_ALIVE)) | (P.msg ? kMsg : 0u);
     for (int o = 0; o < 2 * a.k; ++o) a.offs[o] = d.offsets[o];
-    hipLaunchKernelGGL(gnca_b_adjoint, dim3(B * P.tps3), dim3(kThreads), P.ldsC, st, a);
+    hipLaunchKernelGGL(gnca_b_adjoint, dim3(B * P.tps3 * a.ncg), dim3(kThreads), P.ldsC, st, a);
     if ((rc = bwd_check()) != GNCA_OK) return rc;
   }
+  const int dmod = std::max(d.d_model, 1);
   {
     Reducer r(pb, false, (long)P.gridB * NW, P.npart);
     r.add(P.o_w1, Hd * 3 * C, 1, grads->w1);
@@ -1609,6 +1615,13 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     if (P.graph) {
       r.add(P.o_wm, C * C, 1, grads->wm);
       r.add(P.o_bm, C, 1, grads->bm);
+      if (!(P.msg && P.zp)) {   // torus (or no message): the offset weights are constants
+        r.add(0, dmod * C, 0, grads->wq);
+        r.add(0, dmod, 0, grads->bq);
+        r.add(0, dmod * C, 0, grads->wk);
+        r.add(0, dmod, 0, grads->bk);
+        r.add(0, 1, 0, grads->scaling);
+      }
     }
     if ((rc = r.launch(st)) != GNCA_OK) return rc;
   }
@@ -1618,15 +1631,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     r.add(3, C, 2, grads->gn_bias);
     if ((rc = r.launch(st)) != GNCA_OK) return rc;
   }
-  if (!P.graph) return GNCA_OK;
-  const int dmod = std::max(d.d_model, 1);
-  if (!(P.msg && P.zp)) {  // torus (or no message): the offset weights are constants
-    if ((rc = zero_grad(grads->wq, (size_t)dmod * C, st)) || (rc = zero_grad(grads->bq, dmod, st)) ||
-        (rc = zero_grad(grads->wk, (size_t)dmod * C, st)) || (rc = zero_grad(grads->bk, dmod, st)) ||
-        (rc = zero_grad(grads->scaling, 1, st)))
-      return rc;
-    return GNCA_OK;
-  }
+  if (!P.graph || !(P.msg && P.zp)) return GNCA_OK;
   double* dots = reinterpret_cast<double*>(wsb + P.off_dots);
   double* pq = reinterpret_cast<double*>(wsb + P.off_pq);
   float* corr = reinterpret_cast<float*>(wsb + P.off_corr);
