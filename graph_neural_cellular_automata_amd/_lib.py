@@ -57,10 +57,20 @@ class Grads(ctypes.Structure):
         "w1", "b1", "w2", "gn_weight", "gn_bias", "wq", "bq", "wk", "bk", "wm", "bm", "scaling")]
 
 
+class DamageDesc(ctypes.Structure):
+    """Mirror of gnca_damage_desc (include/gnca.h)."""
+    _fields_ = [("B", ctypes.c_int32), ("C", ctypes.c_int32), ("H", ctypes.c_int32), ("W", ctypes.c_int32),
+                ("kind", ctypes.c_int32), ("size", ctypes.c_int32), ("p", ctypes.c_float),
+                ("alpha_thr", ctypes.c_float), ("softness", ctypes.c_float), ("sigma", ctypes.c_float)]
+
+
+DMG_SQUARE, DMG_CIRCLE, DMG_STRIPE_H, DMG_STRIPE_V = 0, 1, 2, 3
+DMG_ALPHA_DROP, DMG_ALPHA_DROP_SOFT, DMG_SALT_PEPPER, DMG_GAUSSIAN, DMG_HIDDEN_NOISE = 4, 5, 6, 7, 8
+
 EXPORTS = ("gnca_abi_version", "gnca_status_string", "gnca_last_hip_error",
            "gnca_workspace_bytes", "gnca_step_f32", "gnca_step_phases_f32", "gnca_message_f32",
            "gnca_perceive_f32", "gnca_rollout_f32", "gnca_bwd_workspace_bytes", "gnca_step_bwd_f32",
-           "gnca_fire_mask_u8", "gnca_step_masked_f32")
+           "gnca_fire_mask_u8", "gnca_step_masked_f32", "gnca_damage_f32")
 
 PHASE_K0, PHASE_K1, PHASE_K2 = 1, 2, 4
 PHASE_ALL = 7
@@ -110,6 +120,8 @@ def load(path: str = LIB_PATH):
     lib.gnca_step_bwd_f32.restype = ctypes.c_int
     lib.gnca_step_bwd_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights), vp, vp, vp,
                                       vp, vp, ctypes.POINTER(Grads), vp, vp, sz, vp]
+    lib.gnca_damage_f32.restype = ctypes.c_int
+    lib.gnca_damage_f32.argtypes = [ctypes.POINTER(DamageDesc), vp, vp, vp, vp]
     lib.gnca_step_masked_f32.restype = ctypes.c_int
     lib.gnca_step_masked_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights), vp, vp, vp,
                                          vp, vp, sz, vp]

@@ -26,6 +26,7 @@
  *   gnca_rollout_f32     the rollout loops that call the step once per CA step, e.g.
  *                        src/training/train_graph_augmented_nca.py:305-321,
  *                        src/testing/test_graph_augmented_regeneration.py:183-194
+ *   gnca_damage_f32      the damage curriculum's batch ops, src/utils/damage.py:15-138
  *   gnca_step_bwd_f32    torch autograd's backward through NeuralCAGraph.forward /
  *                        NeuralCA.forward, i.e. the per-step part of the trainers'
  *                        loss.backward() (BPTT): src/training/train_graph_augmented_nca.py:369,
@@ -214,6 +215,38 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
                       const void* fire, const uint8_t* active, const float* gy, float* gx,
                       const gnca_grads* grads, const void* saved, void* ws, size_t ws_bytes,
                       void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Step-adjacent batch op: damage (src/utils/damage.py:15-138).  ONE damage kind for the whole
+ * batch, in place on the [B,C,H,W] state, with the random draws supplied by the caller (device
+ * memory), so a whole batch is one launch with no host round trip per sample.
+ * -------------------------------------------------------------------------------------------*/
+#define GNCA_DMG_SQUARE       0  /* cutout_square_:  zero all channels of [y,y+size) x [x,x+size)      */
+#define GNCA_DMG_CIRCLE       1  /* cutout_circle_:  zero all channels where (i-cy)^2+(j-cx)^2 <= r^2  */
+#define GNCA_DMG_STRIPE_H     2  /* stripe_wipe_ "h": zero rows [y0, y0+width) (pos[b] = (y0, 0))       */
+#define GNCA_DMG_STRIPE_V     3  /* stripe_wipe_ "v": zero cols [x0, x0+width) (pos[b] = (0, x0))       */
+#define GNCA_DMG_ALPHA_DROP   4  /* alpha_dropout_(hard): zero all channels where u<p and alpha>thr     */
+#define GNCA_DMG_ALPHA_DROP_SOFT 5 /* alpha_dropout_(hard=False): alpha only                            */
+#define GNCA_DMG_SALT_PEPPER  6  /* salt_pepper_alpha_: alpha *= (u >= p)                               */
+#define GNCA_DMG_GAUSSIAN     7  /* gaussian_hole_: all channels *= clamp(1-exp(-r^2/(2(R*soft)^2)),0,1) */
+#define GNCA_DMG_HIDDEN_NOISE 8  /* hidden_scramble_: hidden = clamp(hidden + sigma*n, 0, 1)          */
+
+typedef struct gnca_damage_desc {
+  int32_t B, C, H, W;
+  int32_t kind;        /* GNCA_DMG_*                                                          */
+  int32_t size;        /* square side, circle / gaussian radius, stripe width                  */
+  float p;             /* alpha_drop / salt_pepper probability                                 */
+  float alpha_thr;     /* alpha_drop: alive threshold                                          */
+  float softness;      /* gaussian                                                             */
+  float sigma;         /* hidden noise scale                                                   */
+} gnca_damage_desc;
+
+/*
+ * pos:   int32 [B,2] per-sample (y, x) / centre (cy, cx) for the geometric kinds, else NULL
+ * noise: fp32 uniforms [B,1,H,W] (alpha kinds) or normals [B,C-4,H,W] (hidden noise), else NULL
+ */
+int gnca_damage_f32(const gnca_damage_desc* desc, float* state, const int32_t* pos,
+                    const float* noise, void* stream);
 
 #ifdef __cplusplus
 }

@@ -16,7 +16,7 @@ def _names(pattern):
 
 def case_names():
     """Forward fixtures (make_golden.py)."""
-    return [n for n in _names("*.npz") if not n.startswith(("grad_", "bptt_"))]
+    return [n for n in _names("*.npz") if not n.startswith(("grad_", "bptt_", "damage_"))]
 
 
 def grad_case_names():
