@@ -16,6 +16,8 @@ VARIANTS = {
     "full": 0, "no_stage": 1, "no_gather": 2, "no_perceive": 4, "no_mfma": 8, "no_store": 16,
     "no_planes": 32, "mfma_only": 1 | 2 | 4 | 16 | 32, "no_mfma_no_store": 8 | 16,
     "stage_only": 2 | 4 | 8 | 16 | 32,
+    "no_fire": 64, "no_zero": 128, "no_reduce": 256,
+    "bare": 2 | 4 | 8 | 16 | 32 | 64 | 128 | 256, "bare_no_stage": 1 | 2 | 4 | 8 | 16 | 32 | 64 | 128 | 256,
 }
 
 
@@ -23,9 +25,10 @@ def build():
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(ROOT, "graph_neural_cellular_automata_amd", "csrc", "gnca_step.hip")
     procs = []
-    for name, bits in VARIANTS.items():
+    for name, bits in list(VARIANTS.items()) + [("prof", None)]:
+        flags = ["-DGNCA_PROFILE"] if bits is None else [f"-DGNCA_ABLATE={bits}"]
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               f"-DGNCA_ABLATE={bits}", f"-I{ROOT}/include", src, "-o", os.path.join(OUT, f"lib_{name}.so")]
+               *flags, f"-I{ROOT}/include", src, "-o", os.path.join(OUT, f"lib_{name}.so")]
         procs.append(subprocess.Popen(cmd, stderr=subprocess.DEVNULL))
         if len(procs) >= 4:
             procs.pop(0).wait()
@@ -73,6 +76,26 @@ def run(reps=15, rounds=3):
     for n, v in res.items():
         v.sort()
         print(f"{n:18s} median {v[len(v)//2]:.3f} ms   min {v[0]:.3f} ms")
+    # phase timers of the profile build (s_memtime cycles summed over each workgroup's tiles)
+    pl = ctypes.CDLL(os.path.join(OUT, "lib_prof.so"))
+    pl.gnca_step_phases_f32.restype = ctypes.c_int
+    pl.gnca_step_phases_f32.argtypes = libs["full"].gnca_step_phases_f32.argtypes
+    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    assert pl.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), x.data_ptr(), out.data_ptr(), None,
+                                   None, ws.data_ptr(), ws.numel(), st.cuda_stream, 2) == 0
+    e1.record(st)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * (1024 * 8))()
+    assert pl.gnca_prof_dump(buf) == 0
+    import numpy as np
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8).astype(np.float64)
+    a = a[a.sum(1) > 0]
+    names = ["dma_issue", "fire+dma_wait", "planes", "compaction", "groups", "reduction", "-", "loop_tail"]
+    tot = a.sum(1).mean()
+    print(f"prof build: {e0.elapsed_time(e1):.3f} ms; mean cycles per workgroup {tot:.0f} over {len(a)} WGs")
+    for i, nm in enumerate(names):
+        print(f"  {nm:14s} {a[:, i].mean():12.0f} cycles  {100 * a[:, i].mean() / tot:5.1f} %")
 
 
 if __name__ == "__main__":
