@@ -50,10 +50,27 @@ constexpr int kAblPerceive = 4;  // skip the 3x3 perception (y = 0)
 constexpr int kAblMfma = 8;      // skip GEMM1/GEMM2 MFMAs
 constexpr int kAblStore = 16;    // skip the dx stores
 constexpr int kAblPlanes = 32;   // skip the alive / sender planes
+constexpr int kAblFire = 64;     // fire = a fixed checkerboard instead of the hash (same density)
+constexpr int kAblZero = 128;    // skip the dead-cell zero stores of the compaction pass
+constexpr int kAblReduce = 256;  // skip the per-tile GroupNorm partial reduction
 constexpr uint32_t kMsgOnly = 1u << 16;   // internal K1 flag: write agg message, skip MLP
 constexpr uint32_t kGraphOn = 1u << 17;   // internal K1 flag: gather + message projection needed
 
 __device__ float g_zero[4];  // LDS-DMA source for off-image cells (zero-initialised)
+
+// Measurement-only phase timers (tools/ablate.py builds with -DGNCA_PROFILE): wave 0 of each K1
+// workgroup accumulates s_memtime deltas per phase; gnca_prof_dump copies them out.
+#ifdef GNCA_PROFILE
+constexpr int kProfPhases = 8;
+__device__ unsigned long long g_prof[1024][kProfPhases];
+#define PROF_DECL unsigned long long prof_t = __builtin_amdgcn_s_memtime(), prof_acc[kProfPhases] = {0};
+#define PROF_MARK(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
+#define PROF_STORE do { if (threadIdx.x == 0) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][i_] = prof_acc[i_]; } while (0)
+#else
+#define PROF_DECL
+#define PROF_MARK(i) do {} while (0)
+#define PROF_STORE do {} while (0)
+#endif
 
 // ------------------------------------------------------------------------------------------
 // LDS layout of K1 (floats; every region starts on a 16-byte boundary)
@@ -281,7 +298,9 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
   const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
   const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
   const int t_begin = xg_ * tq + min(xg_, trm), t_end = t_begin + tq + (xg_ < trm ? 1 : 0);
+  PROF_DECL
   for (int tile = t_begin + xr_; tile < t_end; tile += per_x) {
+    PROF_MARK(7);   // loop back-edge / tail of the previous tile
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
@@ -352,6 +371,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
                                          4, 0, 0);
       }
     }
+    PROF_MARK(0);   // DMA issue
     // ---- per-tile side tables while the DMA is in flight: offset weights, fire plane ----
     if (graph_on && !uniform_w)
       for (int o = tid; o < kp; o += NT)
@@ -367,12 +387,14 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
       else if (a.fire_mode == GNCA_FIRE_MASK_U8)
         fire = reinterpret_cast<const uint8_t*>(a.fire)[(size_t)b * HW + cell] != 0;
       else if (a.fire_mode == GNCA_FIRE_HASH)
-        fire = hash_uniform(a.seed, a.rng_step, (uint64_t)(a.sample_base + b), cell) <= a.fire_rate;
+        fire = (GNCA_ABLATE & kAblFire) ? ((cell & 1) != 0)
+                                        : hash_uniform(a.seed, a.rng_step, (uint64_t)(a.sample_base + b), cell) <= a.fire_rate;
       fp[n] = fire ? 1.f : 0.f;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
+    PROF_MARK(1);   // fire plane + DMA wait + barrier
     // ---- alive masks (max_pool 3x3 > thr, image-bounded, ncagraph.py:85-92): the sender plane
     //      (alive_to_alive ? A_graph : 1, zero where the source is off-image) over the region, and
     //      keep = pre-update alive AND fire for the tile cells ----
@@ -415,6 +437,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
     //      its MLP / message work is skipped and its zeros are stored here.  The live cells are
     //      listed in cell order (wave ballots, fixed order: deterministic) and packed 16 per MFMA
     //      group.  Off for the message-only and attention calls, which need every cell. ----
+    PROF_MARK(2);   // planes + barrier
     int* lst = reinterpret_cast<int*>(smem + L.lst);
     int* wcnt = lst + r4(TH * TW);
     int nlive = 0;
@@ -437,13 +460,15 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
           lst[off + pre] = n;
         } else if (inb) {
           float* oz = a.out + (size_t)b * C * HW + cell0 + (size_t)ti * W + tj;
-          for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
+          if (!(GNCA_ABLATE & kAblZero))
+            for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
         }
         nlive += tot;
         __syncthreads();   // wcnt is rewritten by the next pass
       }
     }
 
+    PROF_MARK(3);   // compaction
     const int qend = compact ? (nlive + 15) >> 4 : (FIXED ? cGPW * NW : ngroups);
 #pragma unroll 1
     for (int q = wave; q < qend; q += NW) {
@@ -664,7 +689,9 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
         }
     }
 
+    PROF_MARK(4);   // group loop
     // ---- per-tile partials: fp64 wave shuffle, then across the waves in LDS ----
+    if (GNCA_ABLATE & kAblReduce) continue;
     double d1 = s1, d2 = s2;
     if (!msg_only) {
       for (int off = 32; off > 0; off >>= 1) {
@@ -703,7 +730,9 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
         a.attn_mm[(size_t)tile * 2 + 1] = mx;
       }
     }
+    PROF_MARK(5);   // per-tile reduction
   }
+  PROF_STORE;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1457,6 +1486,12 @@ int gnca_perceive_f32(int32_t B, int32_t C, int32_t H, int32_t W, const float* w
                      reinterpret_cast<hipStream_t>(stream), B, C, H, W, weight, x, y);
   return check_launch();
 }
+
+#ifdef GNCA_PROFILE
+int gnca_prof_dump(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int gnca_fire_mask_u8(const gnca_step_desc* desc, uint8_t* mask, void* stream) {
   if (!desc || !mask || desc->B <= 0 || desc->H <= 0 || desc->W <= 0) return GNCA_ERR_INVALID;
