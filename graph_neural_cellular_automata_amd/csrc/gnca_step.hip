@@ -31,6 +31,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <mutex>
 #include <type_traits>
 #include <unordered_map>
@@ -1089,6 +1090,8 @@ struct Plan {
 
 static int max_lds_bytes() { return 160 * 1024; }
 
+static int device_cus();
+
 static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   if (!d || d->B <= 0 || d->C < 4 || d->H <= 0 || d->W <= 0 || d->hidden <= 0) return false;
   if (d->num_offsets < 0 || d->num_offsets > GNCA_MAX_OFFSETS) return false;
@@ -1117,6 +1120,8 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // GNCA_K1_TILE=<TH>x<TW> restricts the fixed variants to one tile shape
   static const bool only256 = getenv("GNCA_K1_NT256") != nullptr;
   static const char* tile_env = getenv("GNCA_K1_TILE");
+  const Variant* fixed_pick = nullptr;
+  long fixed_tiles = 0;
   for (const Variant& v : kVariants) {
     if (v.TH == 0 || v.CP != CP || v.HDP != HDP || d->C != CP || msg_only || attn_on) continue;
     if (only256 && v.NT > kThreads) continue;
@@ -1129,12 +1134,26 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
     const K1Layout L = k1_layout(CP, HDP, v.TH, v.TW, v.RY, v.RX, P->k);
     // LDS per workgroup: 80 KB for two 256-thread workgroups per CU, 160 KB for one of 512
     if ((size_t)L.total * 4 > (v.NT >= 512 ? (size_t)max_lds_bytes() : 80 * 1024)) continue;
-    P->var = &v;
-    P->RY = v.RY;
-    P->RX = v.RX;
-    ry = v.RY;
-    rx = v.RX;
-    break;
+    // list order is the large-batch preference (big tiles amortise the per-tile work); a batch
+    // too small to give every CU two workgroups' worth of tiles takes the variant with the most
+    // tiles instead (measured at B=8, 72^2: 24x36 55 us/step, 8x24 43 us/step)
+    const long tiles = (long)d->B * (d->H / v.TH) * (d->W / v.TW);
+    const long fill = 2L * device_cus() * (512 / v.NT);
+    if (!fixed_pick) {
+      fixed_pick = &v;
+      fixed_tiles = tiles;
+      if (tiles >= fill) break;   // large batch: first (preferred) eligible variant
+    } else if (tiles > fixed_tiles) {
+      fixed_pick = &v;
+      fixed_tiles = tiles;
+    }
+  }
+  if (fixed_pick) {
+    P->var = fixed_pick;
+    P->RY = fixed_pick->RY;
+    P->RX = fixed_pick->RX;
+    ry = fixed_pick->RY;
+    rx = fixed_pick->RX;
   }
   // tile choice: fewest padded cells + staged halo, LDS <= 80 KB (2 workgroups / CU) if possible
   static const int ths[] = {4, 8, 12, 16, 24};
@@ -1172,7 +1191,9 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // K2 bands: ~6 row bands per sample (many small workgroups: no wave-quantisation tail),
   // each with its alpha rows + 2 halo rows and its post mask in LDS (<= 48 KB)
   {
-    long rows = (d->H + 5) / 6;
+    // ~6 bands per sample; more (thinner) bands when the batch is too small to fill the chip
+    const long nb_target = std::max<long>(6, (2L * device_cus() + d->B - 1) / d->B);
+    long rows = (d->H + nb_target - 1) / nb_target;
     static const char* band_env = getenv("GNCA_K2_BAND");   // measurement knob (A/B runs only)
     if (band_env && atoi(band_env) > 0) rows = atoi(band_env);
     const long cap = (48L * 1024 / 4 / d->W - 2) / 2;
