@@ -89,6 +89,14 @@ __host__ __device__ constexpr bool w1_in_regs(int, int) { return false; }
 // LDS-DMA wave-instructions of 64 dwords, plane stride PSTR >= 64*NI and = 16 mod 32), plus one
 // alpha plane with one more ring ((RH+2) x (RW+2), NIA instructions) for the 3x3 alive max-pool of
 // the gather sources and the Sobel-ring cells.
+// Channel-plane stride of the staged region: a multiple of the DMA chunk (64 dwords, or 256 floats
+// for the 16-byte DMA of quad-aligned regions) plus 16 floats, so the planes start 16 banks apart.
+__host__ __device__ constexpr int k1_pstr(int RH, int RW, int RX, int TW) {
+  return ((RW % 4) == 0 && (RX % 4) == 0 && (TW % 4) == 0)
+             ? 256 * ((RH * RW / 4 + 63) / 64) + 16
+             : 64 * ((RH * RW + 63) / 64) + 16;
+}
+
 __host__ __device__ inline K1Layout k1_layout(int CP, int HDP, int TH, int TW, int RY, int RX,
                                               int kmax) {
   K1Layout L;
@@ -97,7 +105,7 @@ __host__ __device__ inline K1Layout k1_layout(int CP, int HDP, int TH, int TW, i
   L.RH = TH + 2 * RY;
   L.RW = TW + 2 * RX;
   L.NI = (L.RH * L.RW + 63) / 64;
-  L.PSTR = 64 * L.NI + 16;
+  L.PSTR = k1_pstr(L.RH, L.RW, RX, TW);
   L.ALW = L.RW + 2;
   L.NIA = ((L.RH + 2) * L.ALW + 63) / 64;
   const int kp = r4(kmax > 0 ? kmax : 4);
@@ -172,7 +180,10 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
   constexpr bool FIXED = TH_ > 0;
   // compile-time region geometry of the fixed instantiations
   constexpr int cRH = TH_ + 2 * RY_, cRW = TW_ + 2 * RX_;
-  constexpr int cNI = (cRH * cRW + 63) / 64, cPSTR = 64 * cNI + 16;
+  constexpr int cNI = (cRH * cRW + 63) / 64, cPSTR = k1_pstr(cRH, cRW, RX_, TW_);
+  // 16-byte LDS-DMA (global_load_lds_dwordx4): region rows of whole, aligned float quads
+  constexpr bool DMA4 = FIXED && (cRW % 4) == 0 && (RX_ % 4) == 0 && (TW_ % 4) == 0;
+  constexpr int cNQ = cRH * cRW / 4, cNI4 = (cNQ + 63) / 64;
   constexpr int cALW = cRW + 2, cNIA = ((cRH + 2) * cALW + 63) / 64;
   constexpr int cGPW = (TH_ * TW_ / 16 + NW - 1) / NW;   // groups per wave per tile (fixed geometry)
   static_assert(!FIXED || (TH_ * TW_) % 16 == 0, "fixed tiles hold whole 16-cell groups");
@@ -319,6 +330,33 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
     //      more ring; torus-wrapped, or a zero source outside the image in pad mode.  No VGPR
     //      round trip; every load of the tile in flight at once. ----
     if (!(GNCA_ABLATE & kAblStage)) {
+      if constexpr (DMA4) {
+        // channel planes by 16-byte DMA: lane quad q = 4 consecutive floats of one region row
+        // (rows hold whole quads; torus wrap keeps a quad contiguous since W % 4 == 0)
+#pragma unroll 1
+        for (int ii_ = wave; ii_ < cNI4; ii_ += NW) {
+          const int q = 64 * ii_ + lane;
+          int off = 0;
+          bool ok = false;
+          if (q < cNQ) {
+            const int e = 4 * q;
+            const int vr = e / cRW, vc = e - (e / cRW) * cRW;
+            int ii = i0 - RY + vr, jj = j0 - RX + vc;
+            while (ii < 0) ii += H; while (ii >= H) ii -= H;
+            while (jj < 0) jj += W; while (jj >= W) jj -= W;
+            off = ii * W + jj;
+            ok = true;
+          }
+          float* dst = xs + 256 * ii_;
+#pragma unroll 4
+          for (int c = 0; c < CP; ++c) {
+            const float* src = ok ? xb + (size_t)c * HW + off : g_zero;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(dst + c * PSTR),
+                                             16, 0, 0);
+          }
+        }
+      } else {
       // channel planes: element e of the (RH x RW) region -> image (i0-RY+vr, j0-RX+vc)
 #pragma unroll 1
       for (int ii_ = wave; ii_ < NI; ii_ += NW) {
@@ -346,6 +384,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
                                            (__attribute__((address_space(3))) void*)(dst + c * PSTR),
                                            4, 0, 0);
         }
+      }
       }
       // alpha plane with one more ring: element e of ((RH+2) x ALW) -> (i0-RY-1+vr, j0-RX-1+vc)
 #pragma unroll 1
