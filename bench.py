@@ -157,6 +157,7 @@ def main_train(args, dev, world, rank):
     from graph_neural_cellular_automata_amd import NeuralCAGraph
     from graph_neural_cellular_automata_amd.dp import allreduce_gradients, normalize_gradients_
     from graph_neural_cellular_automata_amd.pool import SamplePool
+    from graph_neural_cellular_automata_amd.loss import loss_premult_rgba
     torch.manual_seed(7)
     random.seed(42)                       # identical offset draws / fire rates on every rank
     model = NeuralCAGraph(C, HD, update_gain=GAIN, alpha_thr=THR, message_gain=MSG_GAIN,
@@ -190,8 +191,7 @@ def main_train(args, dev, world, rank):
             state = model(state, fire_rate=fr, active=nsteps > t)
         model.message_gain = MSG_GAIN
         cells[0] += int(nsteps.sum().item()) * H * H
-        rgba = torch.cat([state[:, :3] * state[:, 3:4], state[:, 3:4]], 1)
-        loss = ((rgba - target[None]) ** 2).mean()
+        loss = loss_premult_rgba(state[:, :4], target[None]).mean()   # fused HIP loss (fwd+bwd)
         opt.zero_grad(set_to_none=True)
         loss.backward()
         allreduce_gradients(params)

@@ -77,10 +77,86 @@ __global__ __launch_bounds__(kThreads) void gnca_damage(const gnca_damage_desc d
   }
 }
 
+// loss_premult_rgba (train_graph_augmented_nca.py:52-61): one workgroup per sample, fixed-order
+// fp64 reduction (deterministic)
+__global__ __launch_bounds__(kThreads) void gnca_loss_fwd(int H, int W, const float* pred, long pbs,
+                                                          const float* tgt, long tbs, float* out) {
+  __shared__ double red[kThreads / 64];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const size_t HW = (size_t)H * W;
+  const float* p = pred + (size_t)b * pbs;
+  const float* t = tgt + (size_t)b * tbs;
+  double acc = 0.0;
+  for (size_t e = tid; e < HW; e += kThreads) {
+    const float a = p[3 * HW + e];
+    float s = 0.f;
+    for (int c = 0; c < 3; ++c) {
+      const float r = p[c * HW + e] * a - t[c * HW + e];
+      s = fmaf(r, r, s);
+    }
+    const float ra = a - t[3 * HW + e];
+    acc += (double)fmaf(ra, ra, s);
+  }
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((tid & 63) == 0) red[tid >> 6] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    double v = 0.0;
+    for (int w = 0; w < kThreads / 64; ++w) v += red[w];
+    out[b] = (float)(v / (4.0 * (double)HW));
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void gnca_loss_bwd(int B, int H, int W, const float* pred, long pbs,
+                                                          const float* tgt, long tbs, const float* g,
+                                                          float* gp, long gbs) {
+  const size_t HW = (size_t)H * W, total = (size_t)B * HW;
+  for (size_t e = (size_t)blockIdx.x * kThreads + threadIdx.x; e < total; e += (size_t)gridDim.x * kThreads) {
+    const size_t b = e / HW, q = e - b * HW;
+    const float* p = pred + b * pbs;
+    const float* t = tgt + b * tbs;
+    float* o = gp + b * gbs;
+    const float s = g[b] * (float)(2.0 / (4.0 * (double)HW));
+    const float a = p[3 * HW + q];
+    float ga = a - t[3 * HW + q];
+    for (int c = 0; c < 3; ++c) {
+      const float x = p[c * HW + q];
+      const float r = x * a - t[c * HW + q];
+      o[c * HW + q] = s * r * a;
+      ga = fmaf(r, x, ga);
+    }
+    o[3 * HW + q] = s * ga;
+  }
+}
+
 }  // namespace
 }  // namespace gnca
 
 using namespace gnca;
+
+extern "C" int gnca_loss_premult_f32(int32_t B, int32_t H, int32_t W, const float* pred, int64_t pbs,
+                                     const float* target, int64_t tbs, float* per_sample, void* stream) {
+  if (B <= 0 || H <= 0 || W <= 0 || !pred || !target || !per_sample) return GNCA_ERR_INVALID;
+  hipLaunchKernelGGL(gnca_loss_fwd, dim3(B), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream), H, W,
+                     pred, (long)pbs, target, (long)tbs, per_sample);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { g_last_hip = (int)e; return GNCA_ERR_HIP; }
+  return GNCA_OK;
+}
+
+extern "C" int gnca_loss_premult_bwd_f32(int32_t B, int32_t H, int32_t W, const float* pred, int64_t pbs,
+                                         const float* target, int64_t tbs, const float* g, float* grad_pred,
+                                         int64_t gbs, void* stream) {
+  if (B <= 0 || H <= 0 || W <= 0 || !pred || !target || !g || !grad_pred) return GNCA_ERR_INVALID;
+  const size_t total = (size_t)B * H * W;
+  size_t blocks = (total + kThreads - 1) / kThreads;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(gnca_loss_bwd, dim3((unsigned)blocks), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                     B, H, W, pred, (long)pbs, target, (long)tbs, g, grad_pred, (long)gbs);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { g_last_hip = (int)e; return GNCA_ERR_HIP; }
+  return GNCA_OK;
+}
 
 extern "C" int gnca_damage_f32(const gnca_damage_desc* d, float* state, const int32_t* pos,
                                const float* noise, void* stream) {

@@ -248,6 +248,21 @@ typedef struct gnca_damage_desc {
 int gnca_damage_f32(const gnca_damage_desc* desc, float* state, const int32_t* pos,
                     const float* noise, void* stream);
 
+/*
+ * The graph trainer's loss (src/training/train_graph_augmented_nca.py:52-61), fused:
+ *   per_sample[b] = mean_{c<4,i,j} (rgba(pred)[b,c,i,j] - target[b,c,i,j])^2,
+ *   rgba(pred) = (pred_rgb * pred_alpha, pred_alpha),
+ * and its backward grad_pred[b,c,i,j] = g[b] * d per_sample[b] / d pred[b,c,i,j] (channels 0..3).
+ * pred / grad_pred are [B,4,H,W] with sample stride `pred_bstride` floats and channel stride H*W
+ * (a channel slice of a contiguous [B,C,H,W] state: pred_bstride = C*H*W); target has sample
+ * stride `target_bstride` (0 = one target broadcast over the batch).  fp64 per-sample sums.
+ */
+int gnca_loss_premult_f32(int32_t B, int32_t H, int32_t W, const float* pred, int64_t pred_bstride,
+                          const float* target, int64_t target_bstride, float* per_sample, void* stream);
+int gnca_loss_premult_bwd_f32(int32_t B, int32_t H, int32_t W, const float* pred, int64_t pred_bstride,
+                              const float* target, int64_t target_bstride, const float* g,
+                              float* grad_pred, int64_t grad_bstride, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
