@@ -1,0 +1,57 @@
+"""Checkpoint round trip in the trainer's format (graph_neural_cellular_automata_amd.checkpoint vs
+train_graph_augmented_nca.py:196-266): payload keys, resume-candidate choice by
+(epoch, global_step), and model/optimizer/scheduler state restored exactly.  The model weights
+are a trained checkpoint's (golden fixture), so the state_dict keys are the reference's own."""
+import torch
+
+from graph_neural_cellular_automata_amd import NeuralCAGraph
+from graph_neural_cellular_automata_amd.checkpoint import (count_parameters, load_checkpoint,
+                                                           pick_resume, save_checkpoint)
+from tests.golden_io import Case
+
+
+def _model():
+    c = Case("grad_graph_zeropad_latest_grown_b2_40")
+    m = NeuralCAGraph(16, graph_zero_padded_shift=True)
+    m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in c.weights.items()}, strict=True)
+    return m
+
+
+def _opt(m):
+    opt = torch.optim.Adam(m.parameters(), lr=2e-3)
+    sch = torch.optim.lr_scheduler.StepLR(opt, step_size=3, gamma=0.5)
+    return opt, sch
+
+
+def test_round_trip_and_resume_choice(tmp_path):
+    m = _model()
+    opt, sch = _opt(m)
+    for p in m.parameters():                      # one optimiser step so Adam has state
+        p.grad = torch.full_like(p, 0.01)
+    opt.step()
+    sch.step()
+    save_checkpoint(tmp_path, "epoch2_last", m, opt, sch, epoch=2, global_step=40, config={"a": 1})
+    save_checkpoint(tmp_path, "ep3_step5_last", m, opt, sch, epoch=3, global_step=45)
+    save_checkpoint(tmp_path, "crash_ep3_step9", m, opt, sch, epoch=3, global_step=49)
+    save_checkpoint(tmp_path, "epoch1_final", m, opt, sch, epoch=1, global_step=20, latest=True)
+    (tmp_path / "nca_epoch9_broken.pt").write_bytes(b"not a checkpoint")
+    path, payload = pick_resume(tmp_path)
+    assert path.endswith("nca_crash_ep3_step9.pt")
+    assert set(payload) == {"epoch", "model_state", "optimizer_state", "scheduler_state", "config",
+                            "param_count", "global_step"}
+    assert payload["param_count"] == count_parameters(m)
+
+    m2 = NeuralCAGraph(16, graph_zero_padded_shift=True)
+    opt2, sch2 = _opt(m2)
+    assert load_checkpoint(payload, m2, opt2, sch2) == 4
+    for (k, a), b in zip(m.state_dict().items(), m2.state_dict().values()):
+        assert torch.equal(a, b), k
+    s1, s2 = opt.state_dict(), opt2.state_dict()
+    for i in s1["state"]:
+        for k in s1["state"][i]:
+            assert torch.equal(torch.as_tensor(s1["state"][i][k]), torch.as_tensor(s2["state"][i][k]))
+    assert sch2.state_dict() == sch.state_dict()
+
+
+def test_empty_dir_has_no_resume(tmp_path):
+    assert pick_resume(tmp_path) == (None, None)
