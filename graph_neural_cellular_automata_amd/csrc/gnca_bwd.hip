@@ -35,6 +35,7 @@
 //                         the caller's gradient buffers (deterministic: no float atomics).
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <unordered_map>
@@ -49,6 +50,20 @@ __device__ float g_bzero[4];   // LDS-DMA source for off-image cells (zero-initi
 constexpr uint32_t kMsg = 1u << 16;      // message path active (k > 0 and message_gain != 0)
 constexpr uint32_t kFirst = 1u << 17;    // first hidden slice: also the message backward
 constexpr uint32_t kGN = 1u << 18;       // GroupNorm on
+
+// Measurement-only phase timers of BB (tools/bprof.py builds with -DGNCA_PROFILE): wave 0 of each
+// workgroup accumulates s_memtime deltas per phase; gnca_bprof_dump copies them out.
+#ifdef GNCA_PROFILE
+constexpr int kBProfPhases = 8;
+__device__ unsigned long long g_bprof[1024][kBProfPhases];
+#define BPROF_DECL unsigned long long prof_t = __builtin_amdgcn_s_memtime(), prof_acc[kBProfPhases] = {0};
+#define BPROF_MARK(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
+#define BPROF_STORE do { if (threadIdx.x == 0) for (int i_ = 0; i_ < kBProfPhases; ++i_) g_bprof[blockIdx.x & 1023][i_] = prof_acc[i_]; } while (0)
+#else
+#define BPROF_DECL
+#define BPROF_MARK(i) do {} while (0)
+#define BPROF_STORE do {} while (0)
+#endif
 
 __host__ __device__ inline int s16(int v) {  // >= v, multiple of 16, == 16 mod 32 (bank spread)
   const int s = (v + 15) & ~15;
@@ -77,11 +92,8 @@ __device__ __forceinline__ double2 block_sum2(double a, double b, double* red) {
 
 __device__ __forceinline__ void sample_stats(const double* stats, int b, int tps, double n, float eps,
                                              float* mu, float* rs) {
-  double t1 = 0.0, t2 = 0.0;  // the forward K2's fixed-order sum (same values bit for bit)
-  for (int t = 0; t < tps; ++t) {
-    t1 += stats[((size_t)b * tps + t) * 2];
-    t2 += stats[((size_t)b * tps + t) * 2 + 1];
-  }
+  double t1, t2;  // the forward K2's fixed-order sum (same values bit for bit)
+  seq_sum2(stats + (size_t)b * tps * 2, tps, 2, &t1, &t2);
   const double m = t1 / n;
   double var = t2 / n - m * m;
   if (var < 0.0) var = 0.0;
@@ -169,34 +181,53 @@ __global__ __launch_bounds__(kThreads) void gnca_b_gnprep(const BAArgs a) {
     post[e] = mx > a.thr ? 1.f : 0.f;
   }
   __syncthreads();
+  // one wave per channel (c = wave, wave + NW, ...): wave-level reductions need no barrier, and
+  // 4 cells per lane are loaded together, so a small band is not a chain of 2C block reductions
   const size_t base = (size_t)r0 * W;
+  const int lane = tid & 63, wave = tid >> 6;
   double su = 0.0, sux = 0.0;
   double* outp = a.part + (size_t)blockIdx.x * (2 + 2 * C);
-  for (int c = 0; c < C; ++c) {
+  for (int c = wave; c < C; c += NW) {
     const float gc = gn ? a.gamma[c] : 1.f, bc = gn ? a.beta[c] : 0.f;
     const float gcr = gc * rs;
     double sg = 0.0, sgx = 0.0;
-    for (int e = tid; e < nb; e += kThreads) {
-      const size_t p = (size_t)c * HW + base + e;
-      const float d = db[p];
-      const float xhat = (d - mu) * rs;
-      const float xn = gn ? (c == 3 ? (d - mu) * rs * gc + bc : (d - mu) * gcr + bc) : d;
-      const float t = tanhf(xn);
-      float g = gb[p];
-      if (c == 3) g *= post[e];                       // x * gate, gate on alpha only (:158-166)
-      gxb[p] = g;                                     // the residual x + ... (:155)
-      const float gxn = g * a.gain * (1.f - t * t);   // tanh(.)*update_gain (:154)
-      const float u = gn ? gxn * gc : gxn;
-      ub[p] = u;
-      sg += (double)gxn;
-      sgx += (double)gxn * (double)xhat;
-      su += (double)u;
-      sux += (double)u * (double)xhat;
+    for (int e0 = 0; e0 < nb; e0 += 4 * 64) {
+      float dv[4], gv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 64 * u + lane;
+        const size_t p = (size_t)c * HW + base + e;
+        dv[u] = e < nb ? db[p] : 0.f;
+        gv[u] = e < nb ? gb[p] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 64 * u + lane;
+        if (e >= nb) continue;
+        const size_t p = (size_t)c * HW + base + e;
+        const float d = dv[u];
+        const float xhat = (d - mu) * rs;
+        const float xn = gn ? (c == 3 ? (d - mu) * rs * gc + bc : (d - mu) * gcr + bc) : d;
+        const float t = tanhf(xn);
+        float g = gv[u];
+        if (c == 3) g *= post[e];                       // x * gate, gate on alpha only (:158-166)
+        gxb[p] = g;                                     // the residual x + ... (:155)
+        const float gxn = g * a.gain * (1.f - t * t);   // tanh(.)*update_gain (:154)
+        const float uu = gn ? gxn * gc : gxn;
+        ub[p] = uu;
+        sg += (double)gxn;
+        sgx += (double)gxn * (double)xhat;
+        su += (double)uu;
+        sux += (double)uu * (double)xhat;
+      }
     }
-    const double2 r = block_sum2(sgx, sg, red);
-    if (tid == 0) {
-      outp[2 + 2 * c] = r.x;
-      outp[3 + 2 * c] = r.y;
+    for (int off = 32; off > 0; off >>= 1) {
+      sg += __shfl_xor(sg, off);
+      sgx += __shfl_xor(sgx, off);
+    }
+    if (lane == 0) {
+      outp[2 + 2 * c] = sgx;
+      outp[3 + 2 * c] = sg;
     }
   }
   const double2 r = block_sum2(su, sux, red);
@@ -216,11 +247,8 @@ __global__ __launch_bounds__(kThreads) void gnca_b_coef(const double* stats, con
   if (use_gn) {
     const double n = (double)C * (double)HW;
     sample_stats(stats, b, tps, n, eps, &mu, &rs);
-    double su = 0.0, sux = 0.0;
-    for (int t = 0; t < nbands; ++t) {
-      su += part[((size_t)b * nbands + t) * (2 + 2 * C)];
-      sux += part[((size_t)b * nbands + t) * (2 + 2 * C) + 1];
-    }
+    double su, sux;
+    seq_sum2(part + (size_t)b * nbands * (2 + 2 * C), nbands, 2 + 2 * C, &su, &sux);
     mu_u = (float)(su / n);
     mu_ux = (float)(sux / n);
   }
@@ -324,6 +352,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   float* percs = smem + L.percs;
   float* wts = smem + L.wts;
 
+  BPROF_DECL
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   const int C = a.C, H = a.H, W = a.W, Hd = a.hidden, h0 = a.h0, k = a.k;
@@ -347,31 +376,31 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     const int f = slot / CP, c = slot - f * CP;
     return (hid < Hd && slot < 3 * CP && c < C) ? a.w1[(size_t)hid * 3 * C + f * C + c] : 0.f;
   };
-  for (int idx = tid; idx < MT * 64 * KSP; idx += kThreads) {   // A[hid][slot], k-step s
+  lds_fill<kThreads, 8>(w1f, MT * 64 * KSP, tid, [&](int idx) {   // A[hid][slot], k-step s
     const int s = idx % KSP, ml = idx / KSP, l = ml & 63, m = ml >> 6;
-    w1f[idx] = s < KS ? w1at(h0 + 16 * m + (l & 15), 4 * s + (l >> 4)) : 0.f;
-  }
-  for (int idx = tid; idx < FT * 64 * S1T; idx += kThreads) {   // A[slot][hid], k-step (m, r)
+    return s < KS ? w1at(h0 + 16 * m + (l & 15), 4 * s + (l >> 4)) : 0.f;
+  });
+  lds_fill<kThreads, 8>(w1t, FT * 64 * S1T, tid, [&](int idx) {   // A[slot][hid], k-step (m, r)
     const int e = idx % S1T, fl = idx / S1T, l = fl & 63, ft = fl >> 6;
     const int m = e >> 2, r = e & 3;
-    w1t[idx] = e < 4 * MT ? w1at(h0 + 16 * m + 4 * (l >> 4) + r, 16 * ft + (l & 15)) : 0.f;
-  }
-  for (int idx = tid; idx < MT * 64 * S2T; idx += kThreads) {   // A[hid][c], k-step (mo, s)
+    return e < 4 * MT ? w1at(h0 + 16 * m + 4 * (l >> 4) + r, 16 * ft + (l & 15)) : 0.f;
+  });
+  lds_fill<kThreads, 8>(w2t, MT * 64 * S2T, tid, [&](int idx) {   // A[hid][c], k-step (mo, s)
     const int e = idx % S2T, ml = idx / S2T, l = ml & 63, m = ml >> 6;
     const int mo = e >> 2, s4 = e & 3;
     const int c = 16 * mo + 4 * (l >> 4) + s4, hid = h0 + 16 * m + (l & 15);
-    w2t[idx] = (e < 4 * MO && c < C && hid < Hd) ? a.w2[(size_t)c * Hd + hid] : 0.f;
-  }
-  for (int idx = tid; idx < 16 * MO * SWM; idx += kThreads) {
+    return (e < 4 * MO && c < C && hid < Hd) ? a.w2[(size_t)c * Hd + hid] : 0.f;
+  });
+  lds_fill<kThreads, 4>(wms, 16 * MO * SWM, tid, [&](int idx) {
     const int co = idx / SWM, ci = idx - co * SWM;
-    wms[idx] = (msg && co < C && ci < C) ? a.wm[co * C + ci] : 0.f;
-  }
-  for (int idx = tid; idx < HB; idx += kThreads) b1s[idx] = h0 + idx < Hd ? a.b1[h0 + idx] : 0.f;
-  for (int idx = tid; idx < 16 * MO; idx += kThreads) bms[idx] = (msg && idx < C) ? a.bm[idx] : 0.f;
-  for (int idx = tid; idx < CP * 36; idx += kThreads) {
+    return (msg && co < C && ci < C) ? a.wm[co * C + ci] : 0.f;
+  });
+  lds_fill<kThreads, 1>(b1s, HB, tid, [&](int idx) { return h0 + idx < Hd ? a.b1[h0 + idx] : 0.f; });
+  lds_fill<kThreads, 1>(bms, 16 * MO, tid, [&](int idx) { return (msg && idx < C) ? a.bm[idx] : 0.f; });
+  lds_fill<kThreads, 4>(percs, CP * 36, tid, [&](int idx) {
     const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
-    percs[idx] = (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
-  }
+    return (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
+  });
   __syncthreads();
   bool sobel;
   {
@@ -391,6 +420,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
 #pragma unroll
   for (int mo = 0; mo < MO; ++mo)
     gainr[mo] = (msg && !(hidden_only && mo == 0 && g == 0)) ? a.message_gain : 0.f;
+  BPROF_MARK(0);   // weights -> LDS
 
   // per-wave accumulators of the whole launch (AGPR-resident)
   f4 aw1[MT][FT], aw2[MO][MT], awm[MO][MO], abm[MO];
@@ -433,6 +463,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     float* dYb = a.dY + (size_t)b * 3 * C * HW;
     float* dGb = a.dG + (size_t)b * C * HW;
     __syncthreads();
+    BPROF_MARK(7);   // loop tail
     if (a.active && !a.active[b]) {   // masked step, inactive sample: every cell is dead
       if (first)
         for (int n = tid; n < ncell; n += kThreads) {
@@ -502,8 +533,10 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
                                      a.sample_base, b, HW, (size_t)i * W + j) ? 1.f : 0.f;
       }
     }
+    BPROF_MARK(1);   // DMA issue + fire plane
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    BPROF_MARK(2);   // DMA wait
     // ---- sender plane over the region, keep = pre-alive AND fire on the tile (as K1) ----
     {
       int jq = j0 - RX + lane;
@@ -569,6 +602,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       nlive += tot;
       __syncthreads();
     }
+    BPROF_MARK(3);   // planes + compaction + dead-cell zero stores
 
 #pragma unroll 1
     for (int q = wave; q < ((nlive + 15) >> 4); q += NW) {
@@ -839,6 +873,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
         }
       }
     }
+    BPROF_MARK(4);   // group loop
   }
 
   // ---- this wave's partial gradients -> its own row (reduced later in a fixed order) ----
@@ -889,6 +924,8 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       }
     }
   }
+  BPROF_MARK(5);   // partial rows -> HBM
+  BPROF_STORE;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -941,15 +978,23 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   float* wts = as_ + TH * TW;                          // [k]
   float* pws = wts + (k > 0 ? k : 1);                  // [C*27] perception weights
   const float* xb = a.x + (size_t)b * C * HW;
-  for (int e = tid; e < C * 27; e += kThreads) pws[e] = a.perc[e];
+  lds_fill<kThreads, 2>(pws, C * 27, tid, [&](int e) { return a.perc[e]; });
   if (msg) {
     for (int o = tid; o < k; o += kThreads) wts[o] = a.offw ? a.offw[(size_t)b * k + o] : a.uniform_w;
     for (int n = tid; n < TH * TW; n += kThreads) {
       const int i = i0 + n / TW, j = j0 + n % TW;
-      float mx = -INFINITY;
-      if (i < H && j < W)
-        for (int u = max(0, i - 1); u <= min(H - 1, i + 1); ++u)
-          for (int v = max(0, j - 1); v <= min(W - 1, j + 1); ++v) mx = fmaxf(mx, xb[3 * HW + (size_t)u * W + v]);
+      float v9[9];   // the 3x3 alpha neighbourhood, all nine loads in flight
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          const int ii = i + u - 1, jj = j + v - 1;
+          v9[3 * u + v] = (i < H && j < W && ii >= 0 && ii < H && jj >= 0 && jj < W)
+                              ? xb[3 * HW + (size_t)ii * W + jj] : -INFINITY;
+        }
+      float mx = v9[0];
+#pragma unroll
+      for (int t = 1; t < 9; ++t) mx = fmaxf(mx, v9[t]);
       as_[n] = a2a ? (mx > a.graph_alpha_thr ? 1.f : 0.f) : 1.f;
     }
   }
@@ -996,15 +1041,33 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
     for (int i = 0; i < kBCStage; ++i)
       if (tid + kThreads * i < SE) dst[tid + kThreads * i] = stg[i];
   };
+  // gx is read-modify-written; its next-channel values are prefetched with the staging loads
+  // (th*tw <= 4*kThreads: at most 4 cells per thread)
+  float gxc[4], gxn[4];
+  auto load_gx = [&](int c, float* dst) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = tid + kThreads * u;
+      const int i = i0 + n / TW, j = j0 + n % TW;
+      dst[u] = (n < TH * TW && i < H && j < W) ? a.gx[((size_t)b * C + c) * HW + (size_t)i * W + j] : 0.f;
+    }
+  };
   load(c_lo);
+  load_gx(c_lo, gxc);
   store(buf0);
   __syncthreads();
   for (int c = c_lo; c < c_hi; ++c) {
     float* cur = ((c - c_lo) & 1) ? buf1 : buf0;
     float* nxt = ((c - c_lo) & 1) ? buf0 : buf1;
-    if (c + 1 < c_hi) load(c + 1);
+    if (c + 1 < c_hi) {
+      load(c + 1);
+      load_gx(c + 1, gxn);
+    }
     const float* pw = pws + c * 27;
-    for (int n = tid; n < TH * TW; n += kThreads) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = tid + kThreads * u;
+      if (n >= TH * TW) continue;
       const int ti = n / TW, tj = n % TW;
       const int i = i0 + ti, j = j0 + tj;
       if (i >= H || j >= W) continue;
@@ -1027,9 +1090,10 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
         }
         acc = fmaf(as_[n], sg, acc);
       }
-      float* p = a.gx + ((size_t)b * C + c) * HW + (size_t)i * W + j;
-      *p += acc;
+      a.gx[((size_t)b * C + c) * HW + (size_t)i * W + j] = gxc[u] + acc;
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) gxc[u] = gxn[u];
     if (c + 1 < c_hi) store(nxt);
     __syncthreads();
   }
@@ -1363,6 +1427,9 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   // (padded cells + staged halo) within 160 KB of LDS
   static const int ths[] = {4, 8, 16};
   static const int tws[] = {8, 16, 24, 32};
+  static const char* tile_env = getenv("GNCA_BB_TILE");   // measurement knob (A/B runs only)
+  int eth = 0, etw = 0;
+  if (tile_env) sscanf(tile_env, "%dx%d", &eth, &etw);
   double best = 1e300;
   P->bb = nullptr;
   for (const BBVariant& v : kBB) {
@@ -1372,6 +1439,7 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
     for (int th : ths)
       for (int tw : tws) {
         if ((th * tw) % 64 || tw + 2 * rx + 2 > 64) continue;   // staging rows fit one wave
+        if (eth && (th != eth || tw != etw)) continue;
         const BBLayout L = bb_layout(P->CP, v.HB, th, tw, ry, rx, P->F.k);
         const size_t bytes = (size_t)L.total * 4;
         if (bytes > 160 * 1024) continue;
@@ -1493,6 +1561,12 @@ struct Reducer {
 using namespace gnca;
 
 extern "C" {
+
+#ifdef GNCA_PROFILE
+int gnca_bprof_dump(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bprof), sizeof(g_bprof)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 size_t gnca_bwd_workspace_bytes(const gnca_step_desc* desc) {
   BwdPlan P;

@@ -51,6 +51,49 @@ __host__ __device__ inline int odd4(int v) {  // round up to 4*odd: conflict-fre
   return ((v >> 2) & 1) ? v : v + 4;
 }
 
+// dst[idx] = f(idx) for idx < n (dst in LDS), U values per thread in flight: a plain strided loop
+// waits out one global-load latency per element (~1 us at one workgroup per CU), which is what
+// dominates a small-batch launch's prologue.
+template <int NT, int U, class F>
+__device__ __forceinline__ void lds_fill(float* dst, int n, int tid, F f) {
+  for (int base = tid; base < n; base += NT * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = base + u * NT;
+      v[u] = idx < n ? f(idx) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = base + u * NT;
+      if (idx < n) dst[idx] = v[u];
+    }
+  }
+}
+
+// Sequential (fixed-order, bit-reproducible) sums of the pairs p[t*stride], p[t*stride+1],
+// t < n, with 8 loads in flight instead of one dependent load per term.
+__device__ __forceinline__ void seq_sum2(const double* p, int n, int stride, double* s0, double* s1) {
+  double a = 0.0, b = 0.0;
+  for (int t0 = 0; t0 < n; t0 += 8) {
+    double va[8], vb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool ok = t0 + u < n;
+      va[u] = ok ? p[(size_t)(t0 + u) * stride] : 0.0;
+      vb[u] = ok ? p[(size_t)(t0 + u) * stride + 1] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (t0 + u < n) {
+        a += va[u];
+        b += vb[u];
+      }
+  }
+  *s0 = a;
+  *s1 = b;
+}
+
 // Where the forward keeps its intermediates in the step workspace (gnca_step.hip:make_plan);
 // the backward recomputes them there.
 struct FwdLayout {

@@ -222,36 +222,33 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
   const bool compact = !msg_only && !want_attn;   // skip cells whose update is masked to zero
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
 
-  // ---- weights -> LDS in MFMA fragment order (once per persistent workgroup) ----
+  // ---- weights -> LDS in MFMA fragment order (once per persistent workgroup; lds_fill keeps
+  //      8 loads per thread in flight) ----
   if (!msg_only) {
-    for (int idx = tid; idx < MT * 64 * KSP; idx += NT) {
+    lds_fill<NT, 8>(w1f, MT * 64 * KSP, tid, [&](int idx) {
       const int s = idx % KSP, ml = idx / KSP, l = ml & 63, m = ml >> 6;
       const int hid = 16 * m + (l & 15), slot = 4 * s + (l >> 4);
       const int f = slot / CP, c = slot - f * CP;
-      float v = 0.f;
-      if (s < KS && hid < Hd && c < C) v = a.w1[(size_t)hid * 3 * C + f * C + c];
-      w1f[idx] = v;
-    }
-    for (int idx = tid; idx < MO * 64 * S2; idx += NT) {
+      return (s < KS && hid < Hd && c < C) ? a.w1[(size_t)hid * 3 * C + f * C + c] : 0.f;
+    });
+    lds_fill<NT, 8>(w2f, MO * 64 * S2, tid, [&](int idx) {
       const int e = idx % S2, ml = idx / S2, l = ml & 63, mo = ml >> 6;
       const int m = e >> 2, r = e & 3;
       const int co = 16 * mo + (l & 15), hid = 16 * m + 4 * (l >> 4) + r;
-      float v = 0.f;
-      if (e < S2r && co < C && hid < Hd) v = a.w2[(size_t)co * Hd + hid];
-      w2f[idx] = v;
-    }
-    for (int idx = tid; idx < HDP; idx += NT) b1s[idx] = idx < Hd ? a.b1[idx] : 0.f;
-    for (int idx = tid; idx < CP * 36; idx += NT) {
+      return (e < S2r && co < C && hid < Hd) ? a.w2[(size_t)co * Hd + hid] : 0.f;
+    });
+    lds_fill<NT, 1>(b1s, HDP, tid, [&](int idx) { return idx < Hd ? a.b1[idx] : 0.f; });
+    lds_fill<NT, 4>(percs, CP * 36, tid, [&](int idx) {
       const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
-      percs[idx] = (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
-    }
+      return (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
+    });
   }
-  for (int idx = tid; idx < MO * 64 * SWM; idx += NT) {
+  lds_fill<NT, 4>(wmf, MO * 64 * SWM, tid, [&](int idx) {
     const int s = idx % SWM, ml = idx / SWM, l = ml & 63, mo = ml >> 6;
     const int co = 16 * mo + (l & 15), c = 4 * s + (l >> 4);
-    wmf[idx] = (graph_on && s < CPQ && co < C && c < C) ? a.wm[co * C + c] : 0.f;
-  }
-  for (int idx = tid; idx < CP; idx += NT) bms[idx] = (graph_on && idx < C) ? a.bm[idx] : 0.f;
+    return (graph_on && s < CPQ && co < C && c < C) ? a.wm[co * C + c] : 0.f;
+  });
+  lds_fill<NT, 1>(bms, CP, tid, [&](int idx) { return (graph_on && idx < C) ? a.bm[idx] : 0.f; });
   __syncthreads();
 
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch)
@@ -819,11 +816,8 @@ __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
   if (tid == 0) {
     float mu = 0.f, rs = 1.f;
     if (a.use_gn) {
-      double t1 = 0.0, t2 = 0.0;  // fixed order: deterministic
-      for (int t = 0; t < a.tps; ++t) {
-        t1 += a.stats[((size_t)b * a.tps + t) * 2];
-        t2 += a.stats[((size_t)b * a.tps + t) * 2 + 1];
-      }
+      double t1, t2;  // fixed order: deterministic
+      seq_sum2(a.stats + (size_t)b * a.tps * 2, a.tps, 2, &t1, &t2);
       const double n = (double)C * (double)HW;
       const double m = t1 / n;
       double var = t2 / n - m * m;

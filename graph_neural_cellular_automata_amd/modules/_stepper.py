@@ -1,11 +1,77 @@
 """Shared forward of NeuralCA / NeuralCAGraph: descriptor + weights -> one HIP step."""
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.nn as nn
 
 from .. import _lib as L
 from .. import step as S
+
+
+class _ParamPack(torch.autograd.Function):
+    """Routes ONE flat gradient to a group of parameters.
+
+    Every step of a rollout hands its parameter gradients to the rollout's shared pack token as
+    one flat tensor, so autograd sums them with one add per step and the parameters'
+    AccumulateGrad runs once per backward instead of once per parameter per step (12 small
+    launches per step at the trainer's size).  The token's value is never read."""
+
+    @staticmethod
+    def forward(ctx, sizes, *params):
+        ctx.set_materialize_grads(False)
+        ctx.sizes = sizes
+        ctx.shapes = [p.shape for p in params]
+        return params[0].new_empty(sum(sizes))
+
+    @staticmethod
+    def backward(ctx, flat):
+        if flat is None:
+            return (None,) * (1 + len(ctx.shapes))
+        return (None, *[g.view(s) for g, s in zip(flat.split(ctx.sizes), ctx.shapes)])
+
+
+class _Pack:
+    """A group of parameters (state_dict names) behind one _ParamPack token."""
+
+    def __init__(self, named):
+        self.names = tuple(n for n, _ in named)
+        self.params = [p for _, p in named]
+        self.sizes = tuple(p.numel() for p in self.params)
+        self.token = _ParamPack.apply(self.sizes, *self.params)
+
+    def views(self, flat):
+        return {n: g.view(p.shape) for n, g, p in zip(self.names, flat.split(self.sizes), self.params)}
+
+
+_PACKS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+_SHORT_TO_NAME = {v: k for k, v in S.GRAD_FIELDS.items()}
+
+
+def param_packs(model: nn.Module, tensors: dict | None = None):
+    """(core, graph) packs of the model's trainable parameters that the step backward produces
+    (GRAD_FIELDS; ``gate_mlp`` and the frozen perception are never in a pack, so they keep
+    ``grad=None`` as in the reference).  ``tensors``: the step's weight tensors by short name
+    (``run_step`` has them already; walking ``named_parameters`` costs ~30 us per step).  Cached
+    per module: the token only routes gradients, so it stays valid across optimiser steps as
+    long as the parameter objects are the same."""
+    if tensors is None:
+        named = [(n, p) for n, p in model.named_parameters() if n in S.GRAD_FIELDS]
+    else:
+        named = [(_SHORT_TO_NAME[k], t) for k, t in tensors.items() if k in _SHORT_TO_NAME]
+    named = [(n, p) for n, p in named if p.requires_grad]
+    hit = _PACKS.get(model)
+    if hit is not None and len(hit[0]) == len(named) and all(a is b for a, (_, b) in zip(hit[0], named)) \
+            and hit[2] == named[0][1].device:
+        return hit[1]
+    core = [(n, p) for n, p in named if not n.startswith("graph.")]
+    graph = [(n, p) for n, p in named if n.startswith("graph.")]
+    packs = (_Pack(core) if core else None, _Pack(graph) if graph else None)
+    _PACKS[model] = (tuple(p for _, p in named), packs, named[0][1].device if named else None)
+    return packs
 
 
 class _StepFn(torch.autograd.Function):
@@ -18,19 +84,21 @@ class _StepFn(torch.autograd.Function):
     reference's per-op activations.  Gradients follow the
     reference's graph of tensors: masks are constants, the perception weight is frozen,
     ``gate_mlp`` is never used (None), and the graph parameters get None when no offsets were
-    drawn (``graph_augmentation.py:141-147`` returns zeros without touching them)."""
+    drawn (``graph_augmentation.py:141-147`` returns zeros without touching them).  Parameter
+    gradients leave as one flat tensor per pack (see ``_ParamPack``), written in place by the
+    backward's reduce kernel."""
 
     @staticmethod
-    def forward(ctx, x, desc, weights, keep, fire, want_attn, names, active, *params):
+    def forward(ctx, x, desc, weights, keep, fire, want_attn, active, core, graph, tok_core, tok_graph):
         ws = S.workspace(desc, x.device)   # kept: the backward reuses its update field
         out, attn = S.step(desc, weights, x, fire=fire, want_attention=want_attn, ws=ws, active=active)
         if attn is not None:
             ctx.mark_non_differentiable(attn)
         ctx.save_for_backward(x)
-        ctx.desc, ctx.weights, ctx.keep, ctx.fire, ctx.names = desc, weights, keep, fire, names
+        ctx.desc, ctx.weights, ctx.keep, ctx.fire = desc, weights, keep, fire
         ctx.ws = ws
         ctx.active = active
-        ctx.params = params
+        ctx.packs = (core, graph)
         return out, attn
 
     @staticmethod
@@ -38,20 +106,26 @@ class _StepFn(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         desc = ctx.desc
         no_graph_use = (desc.flags & L.GRAPH) and desc.num_offsets == 0
-        need = ctx.needs_input_grad[8:]
-        want = {}
-        for name, p, nd in zip(ctx.names, ctx.params, need):
-            if not nd or name not in S.GRAD_FIELDS:
+        want, views, flats = {}, {}, [None, None]
+        for i, pack in enumerate(ctx.packs):
+            if pack is None or not ctx.needs_input_grad[9 + i] or (i == 1 and no_graph_use):
                 continue
-            if no_graph_use and name.startswith("graph."):
-                continue
-            want[name] = p
-        gx, grads = S.step_backward(desc, ctx.weights, x, gout.contiguous(), fire=ctx.fire, want=want,
-                                    saved=ctx.ws, active=ctx.active)
+            flats[i] = torch.empty(sum(pack.sizes), dtype=torch.float32, device=x.device)
+            views.update(pack.views(flats[i]))
+            want.update(zip(pack.names, pack.params))
+        gx, _ = S.step_backward(desc, ctx.weights, x, gout.contiguous(), fire=ctx.fire, want=want,
+                                saved=ctx.ws, active=ctx.active, out=views)
         ctx.ws = None
-        pgrads = [grads.get(n) for n in ctx.names]
-        return (gx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, None,
-                *pgrads)
+        return (gx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, None, None,
+                flats[0], flats[1])
+
+
+def apply_step(model: nn.Module, x, desc, weights, keep, fire, want_attn=False, active=None, tensors=None):
+    """One differentiable step: the HIP forward, and the HIP backward into the model's packs."""
+    core, graph = param_packs(model, tensors)
+    tc = core.token if core is not None else None
+    tg = graph.token if graph is not None else None
+    return _StepFn.apply(x, desc, weights, keep, fire, want_attn, active, core, graph, tc, tg)
 
 
 def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen, message_gain,
@@ -93,11 +167,8 @@ def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen,
                        graph_alpha_thr=graph_thr, message_gain=message_gain,
                        fire_rate=fire_rate, fire_mode=fire_mode, gn_eps=eps)
     w, keep = S.make_weights(tensors)
-    named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
-    if torch.is_grad_enabled() and (x.requires_grad or named):
-        names = tuple(n for n, _ in named)
-        params = [p for _, p in named]
-        out, attn = _StepFn.apply(x, desc, w, keep, fire, return_attention, names, active, *params)
+    if torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in tensors.values())):
+        out, attn = apply_step(model, x, desc, w, keep, fire, return_attention, active, tensors)
     else:
         out, attn = S.step(desc, w, x, fire=fire, want_attention=return_attention, active=active)
     return out, attn

@@ -185,20 +185,26 @@ GRAD_FIELDS = {
 }
 
 
-def step_backward(desc, weights, x, gy, fire=None, want: dict | None = None, saved=None, active=None):
+def step_backward(desc, weights, x, gy, fire=None, want: dict | None = None, saved=None, active=None,
+                  out: dict | None = None):
     """Vector-Jacobian product of one step (gnca_step_bwd_f32).
 
     ``want`` maps state_dict names (GRAD_FIELDS keys) to the parameter tensors whose gradients
     are wanted; returns ``(gx, {name: grad})`` with grads shaped like the parameters.
     ``saved``: the workspace of the forward ``step(..., ws=saved)`` call on the same inputs
-    (skips recomputing the forward's update field)."""
+    (skips recomputing the forward's update field).  ``out``: preallocated float32 gradient
+    tensors (e.g. views of one flat buffer) for some of the ``want`` names."""
     lib = L.load()
     gy = _dev_f32(gy, "grad_output")
     gx = torch.empty_like(x)
     g = L.Grads()
-    out = {}
+    given, out = out or {}, {}
     for name, p in (want or {}).items():
-        t = torch.empty(p.shape, dtype=torch.float32, device=x.device)
+        t = given.get(name)
+        if t is None:
+            t = torch.empty(p.shape, dtype=torch.float32, device=x.device)
+        elif t.shape != p.shape or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"gradient buffer for {name} must be contiguous float32 {tuple(p.shape)}")
         out[name] = t
         setattr(g, GRAD_FIELDS[name], t.data_ptr())
     n = lib.gnca_bwd_workspace_bytes(ctypes.byref(desc))
