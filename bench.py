@@ -7,7 +7,8 @@ Per-step host work (the Python ``random.sample`` offset draw, same seed on every
 the timed region.  Weights: the reference's trained nca_latest.pt (carried by the committed golden
 fixture); state: synthetic (RGB, alpha ~ U(0,1), hidden ~ N(0,1)).  Fire masks come from the
 counter RNG keyed by global sample index, so the N-GPU run computes exactly the states the
-1-GPU run would for the same samples.
+1-GPU run would for the same samples.  ``--config c2|c3|c5`` runs the other BASELINE.json GPU
+configs (classic B=8; graph B=8; 32ch 128^2 r=5 K=16) with the same harness.
 
 Multi-GPU: one process per GPU (torchrun), B samples per rank (weak scaling), no collective on
 the data path; barrier + synchronize around the timed region, max time over ranks.
@@ -31,16 +32,37 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-C, HD, D_MODEL, R, K = 16, 128, 16, 4, 8
+HD, D_MODEL = 128, 16
 GAIN, THR, MSG_GAIN, FIRE = 0.05, 0.12, 0.25, 0.5
-FLOP_PER_CELL = 2 * (3 * C * HD + HD * C + C * C)      # 16,896 MFMA FLOP / cell-update
-BYTES_PER_CELL = 2 * C * 4                             # 128 B: read x, write x' (fp32)
 PEAK_F32_MFMA = 157.3e12                               # MI355X_MICROARCH.md, FP32 matrix
 PEAK_HBM = 8.0e12
-FIXTURE = os.path.join(ROOT, "tests", "golden", "graph_torus_latest_grown_b1_72.npz")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+# BASELINE.json configs as bench workloads (SURVEY.md §8d "configs restated").  "headline" is the
+# roofline headline (north_star: B=1024 x 16ch x 72^2 on 1 GPU; weak scaling over GPUs) and the
+# default; c2/c3/c5 are the other GPU configs.  Weights: the reference's trained checkpoints
+# (classic nca_epoch980.pt, graph nca_latest.pt) or, for C=32, the seeded random init with
+# W2 ~ N(0, 0.02), all carried by committed golden fixtures.
+WORKLOADS = {
+    "headline": dict(graph=True, C=16, H=72, B=1024, R=4, K=8,
+                     fixture="graph_torus_latest_grown_b1_72",
+                     name="graph-augmented NCA rollout, torus, r=4, K=8, fire 0.5"),
+    "c2": dict(graph=False, C=16, H=72, B=8, R=0, K=0, fixture="classic_ep980_b2_32",
+               name="classic NCA rollout (BASELINE config 2), fire 0.5"),
+    "c3": dict(graph=True, C=16, H=72, B=8, R=4, K=8, fixture="graph_torus_latest_grown_b1_72",
+               name="graph-augmented NCA rollout (BASELINE config 3), torus, r=4, K=8, fire 0.5"),
+    "c5": dict(graph=True, C=32, H=128, B=128, R=5, K=16, fixture="graph_torus_c32_r5_k16_b1_48",
+               name="graph-augmented NCA rollout (BASELINE config 5), 32ch, torus, r=5, K=16, "
+                    "fire 0.5, pool 1024 sharded 128/GPU"),
+}
 # per-launch HBM traffic of K1/K2 measured by rocprofv3 PMC counters in separate passes
 # (tools/pmc.sh + tools/pmc_traffic.py); counters cannot be read from inside this process
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def flop_per_cell(wl):
+    """MFMA FLOP per cell-update: 2*(3C*Hd + Hd*C + C*C); classic has no C*C."""
+    C = wl["C"]
+    return 2 * (3 * C * HD + HD * C + (C * C if wl["graph"] else 0))
 
 
 def pmc_traffic(kernel):
@@ -57,8 +79,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=96)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=1024, help="samples per GPU")
-    ap.add_argument("--size", type=int, default=72)
+    ap.add_argument("--config", default="headline", choices=sorted(WORKLOADS),
+                    help="rollout workload (BASELINE.json configs); default: the roofline headline")
+    ap.add_argument("--batch", type=int, default=None, help="samples per GPU (default: the config's)")
+    ap.add_argument("--size", type=int, default=None, help="canvas (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="wall budget of the CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -72,34 +96,37 @@ def parse():
     return ap.parse_args()
 
 
-def load_weights(dev):
-    z = np.load(FIXTURE, allow_pickle=False)
-    w = {k[2:]: torch.from_numpy(z[k]).to(dev) for k in z.files if k.startswith("w:")}
-    return w
+def load_weights(dev, wl=None):
+    wl = wl or WORKLOADS["headline"]
+    z = np.load(os.path.join(GOLDEN, wl["fixture"] + ".npz"), allow_pickle=False)
+    return {k[2:]: torch.from_numpy(z[k]).to(dev) for k in z.files if k.startswith("w:")}
 
 
-def weight_struct(w):
+def weight_struct(w, wl):
     from graph_neural_cellular_automata_amd import step as S
     t = dict(perception=w["perception.conv.weight"], w1=w["update_net.0.weight"],
              b1=w["update_net.0.bias"], w2=w["update_net.2.weight"], gn_weight=w["norm.weight"],
-             gn_bias=w["norm.bias"], wq=w["graph.query_proj.weight"], bq=w["graph.query_proj.bias"],
-             wk=w["graph.key_proj.weight"], bk=w["graph.key_proj.bias"], wm=w["graph.msg_proj.weight"],
-             bm=w["graph.msg_proj.bias"], scaling=w["graph.scaling"])
+             gn_bias=w["norm.bias"])
+    if wl["graph"]:
+        t.update(wq=w["graph.query_proj.weight"], bq=w["graph.query_proj.bias"],
+                 wk=w["graph.key_proj.weight"], bk=w["graph.key_proj.bias"],
+                 wm=w["graph.msg_proj.weight"], bm=w["graph.msg_proj.bias"], scaling=w["graph.scaling"])
     return S.make_weights(t)
 
 
-def make_desc(B, H, W, offsets, rank, step0=0):
+def make_desc(wl, B, H, W, offsets, rank, step0=0):
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
-    return S.make_desc(B=B, C=C, H=H, W=W, hidden=HD, d_model=D_MODEL, offsets=offsets,
-                       flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+    flags = L.USE_GROUPNORM | ((L.GRAPH | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE) if wl["graph"] else 0)
+    return S.make_desc(B=B, C=wl["C"], H=H, W=W, hidden=HD, d_model=D_MODEL,
+                       offsets=offsets if wl["graph"] else [], flags=flags,
                        update_gain=GAIN, alpha_thr=THR, message_gain=MSG_GAIN, fire_rate=FIRE,
                        fire_mode=L.FIRE_HASH, rng_seed=42, rng_step=step0, sample_base=rank * B)
 
 
-def cpu_baseline(budget_s: float):
-    """The numpy oracle (float32, the reference's arithmetic) on host cores: B=8 x 72^2 graph
-    steps until the wall budget is spent (>= 2 steps)."""
+def cpu_baseline(budget_s: float, wl, H: int):
+    """The numpy oracle (float32, the reference's arithmetic) on host cores: a B<=8 sample of the
+    same workload, stepped until the wall budget is spent (>= 2 steps)."""
     from oracle import nca_oracle as O
     try:
         from threadpoolctl import threadpool_limits
@@ -107,21 +134,22 @@ def cpu_baseline(budget_s: float):
         threadpool_limits = None
     ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     threads = max(1, min(16, ncpu))
-    z = np.load(FIXTURE, allow_pickle=False)
+    z = np.load(os.path.join(GOLDEN, wl["fixture"] + ".npz"), allow_pickle=False)
     p = {k[2:]: z[k].astype(np.float32) for k in z.files if k.startswith("w:")}
-    cfg = dict(update_gain=GAIN, alpha_thr=THR, use_groupnorm=True, graph=True,
+    cfg = dict(update_gain=GAIN, alpha_thr=THR, use_groupnorm=True, graph=wl["graph"],
                message_gain=MSG_GAIN, hidden_only=True, zero_padded_shift=False, alive_to_alive=True)
+    C = wl["C"]
     rng = np.random.default_rng(0)
-    B, H = 8, 72
+    B = min(8, wl["B"])
     x = rng.random((B, C, H, H), dtype=np.float32)
     x[:, 4:] = rng.standard_normal((B, C - 4, H, H), dtype=np.float32)
-    offs = O.build_offsets(R)
+    offs = O.build_offsets(wl["R"]) if wl["graph"] else []
     rr = random.Random(42)
     ctx = threadpool_limits(limits=threads) if threadpool_limits else None
     steps = 0
     t0 = time.perf_counter()
     while True:
-        chosen = rr.sample(offs, K)
+        chosen = rr.sample(offs, wl["K"]) if wl["graph"] else None
         fm = O.hash_fire_mask(42, steps, 0, B, H, H, FIRE)
         x = O.nca_step(x, p, cfg, chosen=chosen, fire_mask=fm)
         steps += 1
@@ -138,9 +166,10 @@ def cpu_baseline(budget_s: float):
                 break
     except OSError:
         pass
+    kind = f"graph torus r={wl['R']} K={wl['K']}" if wl["graph"] else "classic"
     return {"value": B * H * H * steps / el, "unit": "cell-updates/s", "cores": threads,
             "kind": "port",
-            "sample": f"numpy float32 oracle (oracle/nca_oracle.py), graph torus C16 72x72 K=8, "
+            "sample": f"numpy float32 oracle (oracle/nca_oracle.py), {kind} C{C} {H}x{H}, "
                       f"B={B}, {steps} steps in {el:.1f}s; BLAS threads={threads}, elementwise "
                       f"single-threaded; host CPU: {cpu}"}
 
@@ -158,12 +187,14 @@ def main_train(args, dev, world, rank):
     from graph_neural_cellular_automata_amd.dp import allreduce_gradients, normalize_gradients_
     from graph_neural_cellular_automata_amd.pool import SamplePool
     from graph_neural_cellular_automata_amd.loss import loss_premult_rgba
+    wl = WORKLOADS["headline"]
+    C, R, K = wl["C"], wl["R"], wl["K"]
     torch.manual_seed(7)
     random.seed(42)                       # identical offset draws / fire rates on every rank
     model = NeuralCAGraph(C, HD, update_gain=GAIN, alpha_thr=THR, message_gain=MSG_GAIN,
                           graph_d_model=D_MODEL, graph_attention_radius=R, graph_num_neighbors=K,
                           graph_zero_padded_shift=False).to(dev)
-    model.load_state_dict({k: v for k, v in load_weights(dev).items()}, strict=False)
+    model.load_state_dict({k: v for k, v in load_weights(dev, wl).items()}, strict=False)
     opt = torch.optim.Adam(model.parameters(), lr=2e-4, weight_decay=1e-5)
     params = [p for p in model.parameters() if p.requires_grad]
     B, H = args.train_batch, args.train_size
@@ -264,15 +295,18 @@ def main():
     from graph_neural_cellular_automata_amd.modules.graph_augmentation import GraphAugmentation
     build_offsets = GraphAugmentation._build_offsets   # row-major (dy, dx) table, graph_aug.py:73-83
 
-    B, H = args.batch, args.size
-    offsets_table = build_offsets(R)
-    w, keep = weight_struct(load_weights(dev))
+    wl = WORKLOADS[args.config]
+    C, R, K, graph = wl["C"], wl["R"], wl["K"], wl["graph"]
+    B = args.batch or wl["B"]
+    H = args.size or wl["H"]
+    offsets_table = build_offsets(R) if graph else []
+    w, keep = weight_struct(load_weights(dev, wl), wl)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(B, C, H, H, device=dev, generator=g)
     x[:, 4:] = torch.randn(B, C - 4, H, H, device=dev, generator=g)
     out = torch.empty_like(x)
     scratch = torch.empty_like(x)
-    desc0 = make_desc(B, H, H, offsets_table[:K], rank)
+    desc0 = make_desc(wl, B, H, H, offsets_table[:K], rank)
     ws = S.workspace(desc0, dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
@@ -281,11 +315,12 @@ def main():
 
     def rollout(n, step0, src, dst):
         flat = []
-        for _ in range(n):   # the per-step host draw (graph_augmentation.py:121), timed
-            for dy, dx in rr.sample(offsets_table, K):
-                flat += [dy, dx]
-        arr = (ctypes.c_int8 * len(flat))(*flat)
-        d = make_desc(B, H, H, offsets_table[:K], rank, step0)
+        if graph:
+            for _ in range(n):   # the per-step host draw (graph_augmentation.py:121), timed
+                for dy, dx in rr.sample(offsets_table, K):
+                    flat += [dy, dx]
+        arr = (ctypes.c_int8 * len(flat))(*flat) if flat else None
+        d = make_desc(wl, B, H, H, offsets_table[:K], rank, step0)
         rc = lib.gnca_rollout_f32(ctypes.byref(d), ctypes.byref(w), n, arr, src.data_ptr(),
                                   dst.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(), sptr)
         L.check(rc, "gnca_rollout_f32")
@@ -314,7 +349,7 @@ def main():
 
     # --- K1 (dominant, MFMA-bound) average duration with HIP events on the launch stream ---
     reps = 20
-    d = make_desc(B, H, H, rr.sample(offsets_table, K), rank, 0)
+    d = make_desc(wl, B, H, H, rr.sample(offsets_table, K) if graph else [], rank, 0)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
     ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
     for r in range(reps):
@@ -336,34 +371,44 @@ def main():
     fm = S.fire_mask(d, dev)
     alive = torch.nn.functional.max_pool2d(out[:, 3:4], 3, 1, 1) > THR
     live_frac = float((alive & (fm != 0)).float().mean())
-    k1_flops = cells * FLOP_PER_CELL
+    fpc = flop_per_cell(wl)
+    k1_flops = cells * fpc
     k2_bytes = cells * C * 4 * 3                   # read x, dx; write x'
-    roof = {"bound": "mfma", "kernel": "gnca_k1_update<16,128>", "achieved": k1_flops / (k1_ms * 1e-3) / 1e12,
+    headline = args.config == "headline"
+    roof = {"bound": "mfma", "kernel": f"gnca_k1_update<{C},{HD}>",
+            "achieved": k1_flops / (k1_ms * 1e-3) / 1e12,
             "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
-            "frac": k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA, "traffic": pmc_traffic("K1"),
+            "frac": k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA,
+            "traffic": pmc_traffic("K1") if headline else None,
             "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, profiles/r01_pmc_traffic.json)",
             "k1_ms": k1_ms, "flop_per_launch": k1_flops,
             "live_fraction": live_frac,
             "executed_frac": live_frac * k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA,
-            "note": "achieved = dense algorithmic FLOPs (16,896 per cell-update, SURVEY.md 8d) / K1 "
+            "note": f"achieved = dense algorithmic FLOPs ({fpc:,} per cell-update, SURVEY.md 8d) / K1 "
                     "time; K1 executes the MLP only for live cells (keep = alive AND fire, the "
                     "others have dx = 0 exactly), so MFMA utilisation = executed_frac"}
     roof_k2 = {"bound": "hbm", "kernel": "gnca_k2_finalize", "achieved": k2_bytes / (k2_ms * 1e-3) / 1e9,
                "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": k2_bytes / (k2_ms * 1e-3) / PEAK_HBM,
-               "k2_ms": k2_ms, "bytes_per_launch": k2_bytes, "traffic": pmc_traffic("K2")}
+               "k2_ms": k2_ms, "bytes_per_launch": k2_bytes,
+               "traffic": pmc_traffic("K2") if headline else None}
 
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(args.cpu_seconds)
+            cpu = cpu_baseline(args.cpu_seconds, wl, H)
+        metric = ("cell-updates/sec (B·H·W·steps) for 16ch 72×72 rollout at 1/2/4/8 MI355X" if C == 16
+                  else f"cell-updates/sec (B·H·W·steps) for {C}ch {H}×{H} rollout")
+        wdesc = ("trained nca_latest.pt" if wl["graph"] and C == 16 else
+                 "trained classic nca_epoch980.pt" if not wl["graph"] else
+                 "seeded random init (W2 ~ N(0,0.02))")
         line = {
-            "metric": "cell-updates/sec (B·H·W·steps) for 16ch 72×72 rollout at 1/2/4/8 MI355X",
+            "metric": metric,
             "value": value, "unit": "cell-updates/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic state (RGB,alpha~U(0,1), hidden~N(0,1)); trained nca_latest.pt "
-                    "weights from the committed golden fixture",
-            "config": {"workload": f"graph-augmented NCA rollout, torus, r={R}, K={K}, fire {FIRE}",
+            "data": f"synthetic state (RGB,alpha~U(0,1), hidden~N(0,1)); {wdesc} weights from the "
+                    f"committed golden fixture",
+            "config": {"workload": wl["name"], "config": args.config,
                        "channels": C, "hidden": HD, "height": H, "width": H,
                        "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}"},
             "roofline": roof, "roofline_k2": roof_k2, "cpu_baseline": cpu,

@@ -52,12 +52,13 @@ def run(reps=15, rounds=3):
         lib.gnca_workspace_bytes.argtypes = [ctypes.POINTER(L.StepDesc)]
         libs[name] = lib
     B, H = 1024, 72
-    w, keep = bench.weight_struct(bench.load_weights(dev))
+    wl = bench.WORKLOADS["headline"]
+    w, keep = bench.weight_struct(bench.load_weights(dev, wl), wl)
     x = torch.rand(B, 16, H, H, device=dev)
     out = torch.empty_like(x)
     from graph_neural_cellular_automata_amd.modules.graph_augmentation import GraphAugmentation
     build_offsets = GraphAugmentation._build_offsets
-    d = bench.make_desc(B, H, H, random.Random(0).sample(build_offsets(4), 8), 0)
+    d = bench.make_desc(wl, B, H, H, random.Random(0).sample(build_offsets(4), 8), 0)
     ws = torch.empty(libs["full"].gnca_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream()
     res = {n: [] for n in libs}
