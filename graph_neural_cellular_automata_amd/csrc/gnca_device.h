@@ -71,6 +71,30 @@ __device__ __forceinline__ void lds_fill(float* dst, int n, int tid, F f) {
   }
 }
 
+// A compile-time-sized LDS fill split into its load half and its store half, so several fills can
+// have ALL their global loads in flight before the first LDS store (one load latency for a whole
+// weight set instead of one per fill batch: the prologue of a small-batch launch).
+template <int NT, int N>
+struct RegFill {
+  static constexpr int U = (N + NT - 1) / NT;
+  float v[U];
+  template <class F>
+  __device__ __forceinline__ void load(int tid, F f) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = tid + u * NT;
+      v[u] = idx < N ? f(idx) : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(float* dst, int tid) const {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = tid + u * NT;
+      if (idx < N) dst[idx] = v[u];
+    }
+  }
+};
+
 // Sequential (fixed-order, bit-reproducible) sums of the pairs p[t*stride], p[t*stride+1],
 // t < n, with 8 loads in flight instead of one dependent load per term.
 __device__ __forceinline__ void seq_sum2(const double* p, int n, int stride, double* s0, double* s1) {

@@ -54,6 +54,8 @@ constexpr int kAblPlanes = 32;   // skip the alive / sender planes
 constexpr int kAblFire = 64;     // fire = a fixed checkerboard instead of the hash (same density)
 constexpr int kAblZero = 128;    // skip the dead-cell zero stores of the compaction pass
 constexpr int kAblReduce = 256;  // skip the per-tile GroupNorm partial reduction
+constexpr int kAblTiles = 512;   // skip the tile loop (times launch + prologue)
+constexpr int kAblFill = 1024;   // skip the weight fill (LDS keeps old data)
 constexpr uint32_t kMsgOnly = 1u << 16;   // internal K1 flag: write agg message, skip MLP
 constexpr uint32_t kGraphOn = 1u << 17;   // internal K1 flag: gather + message projection needed
 
@@ -222,33 +224,50 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
   const bool compact = !msg_only && !want_attn;   // skip cells whose update is masked to zero
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
 
-  // ---- weights -> LDS in MFMA fragment order (once per persistent workgroup; lds_fill keeps
-  //      8 loads per thread in flight) ----
-  if (!msg_only) {
-    lds_fill<NT, 8>(w1f, MT * 64 * KSP, tid, [&](int idx) {
-      const int s = idx % KSP, ml = idx / KSP, l = ml & 63, m = ml >> 6;
-      const int hid = 16 * m + (l & 15), slot = 4 * s + (l >> 4);
-      const int f = slot / CP, c = slot - f * CP;
-      return (s < KS && hid < Hd && c < C) ? a.w1[(size_t)hid * 3 * C + f * C + c] : 0.f;
+  // ---- weights -> LDS in MFMA fragment order (once per persistent workgroup).  Every load of
+  //      the whole weight set is issued before the first LDS store: one global-load latency for
+  //      the prologue, which is most of a small-batch launch. ----
+  {
+    RegFill<NT, MT * 64 * KSP> fw1;
+    RegFill<NT, MO * 64 * S2> fw2;
+    RegFill<NT, HDP> fb1;
+    RegFill<NT, CP * 36> fpc;
+    RegFill<NT, MO * 64 * SWM> fwm;
+    RegFill<NT, CP> fbm;
+    if (!msg_only && !(GNCA_ABLATE & kAblFill)) {
+      fw1.load(tid, [&](int idx) {
+        const int s = idx % KSP, ml = idx / KSP, l = ml & 63, m = ml >> 6;
+        const int hid = 16 * m + (l & 15), slot = 4 * s + (l >> 4);
+        const int f = slot / CP, c = slot - f * CP;
+        return (s < KS && hid < Hd && c < C) ? a.w1[(size_t)hid * 3 * C + f * C + c] : 0.f;
+      });
+      fw2.load(tid, [&](int idx) {
+        const int e = idx % S2, ml = idx / S2, l = ml & 63, mo = ml >> 6;
+        const int m = e >> 2, r = e & 3;
+        const int co = 16 * mo + (l & 15), hid = 16 * m + 4 * (l >> 4) + r;
+        return (e < S2r && co < C && hid < Hd) ? a.w2[(size_t)co * Hd + hid] : 0.f;
+      });
+      fb1.load(tid, [&](int idx) { return idx < Hd ? a.b1[idx] : 0.f; });
+      fpc.load(tid, [&](int idx) {
+        const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
+        return (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
+      });
+    }
+    fwm.load(tid, [&](int idx) {
+      const int s = idx % SWM, ml = idx / SWM, l = ml & 63, mo = ml >> 6;
+      const int co = 16 * mo + (l & 15), c = 4 * s + (l >> 4);
+      return (graph_on && s < CPQ && co < C && c < C) ? a.wm[co * C + c] : 0.f;
     });
-    lds_fill<NT, 8>(w2f, MO * 64 * S2, tid, [&](int idx) {
-      const int e = idx % S2, ml = idx / S2, l = ml & 63, mo = ml >> 6;
-      const int m = e >> 2, r = e & 3;
-      const int co = 16 * mo + (l & 15), hid = 16 * m + 4 * (l >> 4) + r;
-      return (e < S2r && co < C && hid < Hd) ? a.w2[(size_t)co * Hd + hid] : 0.f;
-    });
-    lds_fill<NT, 1>(b1s, HDP, tid, [&](int idx) { return idx < Hd ? a.b1[idx] : 0.f; });
-    lds_fill<NT, 4>(percs, CP * 36, tid, [&](int idx) {
-      const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
-      return (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
-    });
+    fbm.load(tid, [&](int idx) { return (graph_on && idx < C) ? a.bm[idx] : 0.f; });
+    if (!msg_only && !(GNCA_ABLATE & kAblFill)) {
+      fw1.store(w1f, tid);
+      fw2.store(w2f, tid);
+      fb1.store(b1s, tid);
+      fpc.store(percs, tid);
+    }
+    fwm.store(wmf, tid);
+    fbm.store(bms, tid);
   }
-  lds_fill<NT, 4>(wmf, MO * 64 * SWM, tid, [&](int idx) {
-    const int s = idx % SWM, ml = idx / SWM, l = ml & 63, mo = ml >> 6;
-    const int co = 16 * mo + (l & 15), c = 4 * s + (l >> 4);
-    return (graph_on && s < CPQ && co < C && c < C) ? a.wm[co * C + c] : 0.f;
-  });
-  lds_fill<NT, 1>(bms, CP, tid, [&](int idx) { return (graph_on && idx < C) ? a.bm[idx] : 0.f; });
   __syncthreads();
 
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch)
@@ -308,7 +327,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
   const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
   const int t_begin = xg_ * tq + min(xg_, trm), t_end = t_begin + tq + (xg_ < trm ? 1 : 0);
   PROF_DECL
-  for (int tile = t_begin + xr_; tile < t_end; tile += per_x) {
+  for (int tile = t_begin + xr_; tile < ((GNCA_ABLATE & kAblTiles) ? t_begin : t_end); tile += per_x) {
     PROF_MARK(7);   // loop back-edge / tail of the previous tile
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
@@ -791,33 +810,84 @@ struct K2Args {
 };
 
 // One workgroup per (sample, band of rows).  LDS: the updated alpha x~_3 over the band + one
-// halo row each side, then the post-update alive mask of the band; the main pass streams
-// (channel, 4-cell) items with 16-byte loads/stores when W % 4 == 0.
-__global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ float sh_norm[4];
-  const int tid = threadIdx.x;
+// halo row each side, then the post-update alive mask of the band.  The main pass streams
+// (channel, cell-vector) items, V = 4 cells (16-byte loads/stores) when W % 4 == 0.  Every load
+// the band needs first (GroupNorm partials, alpha rows, gamma/beta and the first KU main items)
+// is issued before the first barrier: a small-batch launch waits out one memory latency, not
+// one per phase.
+template <int V>
+__device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_norm) {
+  typedef float vf __attribute__((ext_vector_type(V)));
+  constexpr int KU = 4;   // main items per thread in flight
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x / a.nbands, band = blockIdx.x - b * a.nbands;
   const int C = a.C, H = a.H, W = a.W;
   const int r0 = band * a.band, r1 = min(H, r0 + a.band);
   const int h0 = max(0, r0 - 1), h1 = min(H, r1 + 1);       // alpha rows incl. halo
   const size_t HW = (size_t)H * W;
-  if (a.active && !a.active[b]) {   // masked step: an inactive sample passes through unchanged
-    const float* xs_ = a.x + (size_t)b * C * HW;
-    float* os_ = a.out + (size_t)b * C * HW;
-    const int nbc = (r1 - r0) * W;
-    for (int it = tid; it < C * nbc; it += kThreads) {
-      const int c = it / nbc, e = it - c * nbc;
-      os_[(size_t)c * HW + (size_t)r0 * W + e] = xs_[(size_t)c * HW + (size_t)r0 * W + e];
-    }
-    return;
-  }
+  const float* xb = a.x + (size_t)b * C * HW;
+  const float* db = a.dx + (size_t)b * C * HW;
+  float* ob = a.out + (size_t)b * C * HW;
+  const bool gn = a.use_gn != 0;
+  const size_t base = (size_t)r0 * W;
+  const int nb = (r1 - r0) * W;
+  const int nv = nb / V, nitems = C * nv;
 
-  if (tid == 0) {
+  float* at = smem;                                  // [(h1-h0) x W] updated alpha
+  float* post = smem + (size_t)(a.band + 2) * W;     // [(r1-r0) x W] post-update alive mask
+  float* gsh = sh_norm + 4;                          // gamma[C], then beta[C] at +32
+
+  // (1) loads: partials (wave 0), gamma/beta, alpha rows, the first main items
+  double p1 = 0.0, p2 = 0.0;
+  if (wave == 0 && gn)
+    for (int t = lane; t < a.tps && t < 64; t += 64) {
+      p1 = a.stats[((size_t)b * a.tps + t) * 2 + 0];
+      p2 = a.stats[((size_t)b * a.tps + t) * 2 + 1];
+    }
+  float gam = 1.f, bet = 0.f;
+  if (gn && tid < C) { gam = a.gamma[tid]; bet = a.beta[tid]; }
+  const int na = (h1 - h0) * W;
+  constexpr int NA = 2;   // alpha elements per thread in flight (band + 2 rows <= 2*256 typical)
+  float ax[NA], ad[NA];
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int e = tid + u * kThreads;
+    if (e < na) {
+      const size_t p = 3 * HW + (size_t)h0 * W + e;
+      ax[u] = xb[p];
+      ad[u] = db[p];
+    }
+  }
+  vf xv[KU], dv[KU];
+  auto load_items = [&](int it0) {
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int it = it0 + u * kThreads;
+      if (it < nitems) {
+        const int c = it / nv, q = it - c * nv;
+        if (c != 3) {
+          const size_t p = (size_t)c * HW + base + (size_t)V * q;
+          xv[u] = *reinterpret_cast<const vf*>(xb + p);
+          dv[u] = *reinterpret_cast<const vf*>(db + p);
+        }
+      }
+    }
+  };
+  load_items(tid);
+
+  // (2) per-sample statistics (fixed order: seq_sum2's, bit-reproducible)
+  if (wave == 0) {
     float mu = 0.f, rs = 1.f;
-    if (a.use_gn) {
-      double t1, t2;  // fixed order: deterministic
-      seq_sum2(a.stats + (size_t)b * a.tps * 2, a.tps, 2, &t1, &t2);
+    if (gn) {
+      double t1 = 0.0, t2 = 0.0;
+      if (a.tps <= 64) {
+        for (int t = 0; t < a.tps; ++t) {
+          t1 += __shfl(p1, t);
+          t2 += __shfl(p2, t);
+        }
+      } else {
+        seq_sum2(a.stats + (size_t)b * a.tps * 2, a.tps, 2, &t1, &t2);
+      }
       const double n = (double)C * (double)HW;
       const double m = t1 / n;
       double var = t2 / n - m * m;
@@ -825,35 +895,38 @@ __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
       mu = (float)m;
       rs = (float)(1.0 / sqrt(var + (double)a.eps));
     }
-    float amn = 0.f, amx = 0.f;
-    if (a.attn) {
-      amn = INFINITY; amx = -INFINITY;
-      for (int t = 0; t < a.tps; ++t) {
-        amn = fminf(amn, a.attn_mm[((size_t)b * a.tps + t) * 2]);
-        amx = fmaxf(amx, a.attn_mm[((size_t)b * a.tps + t) * 2 + 1]);
+    if (lane == 0) {
+      float amn = 0.f, amx = 0.f;
+      if (a.attn) {
+        amn = INFINITY; amx = -INFINITY;
+        for (int t = 0; t < a.tps; ++t) {
+          amn = fminf(amn, a.attn_mm[((size_t)b * a.tps + t) * 2]);
+          amx = fmaxf(amx, a.attn_mm[((size_t)b * a.tps + t) * 2 + 1]);
+        }
       }
+      sh_norm[0] = mu; sh_norm[1] = rs; sh_norm[2] = amn; sh_norm[3] = amx;
     }
-    sh_norm[0] = mu; sh_norm[1] = rs; sh_norm[2] = amn; sh_norm[3] = amx;
   }
+  if (tid < C) { gsh[tid] = gam; gsh[32 + tid] = bet; }
   __syncthreads();
   const float mu = sh_norm[0], rs = sh_norm[1];
-  const float* xb = a.x + (size_t)b * C * HW;
-  const float* db = a.dx + (size_t)b * C * HW;
-  float* ob = a.out + (size_t)b * C * HW;
-  const bool gn = a.use_gn != 0;
-  const float g3 = gn ? a.gamma[3] : 1.f, b3 = gn ? a.beta[3] : 0.f;
+  const float g3 = gn ? gsh[3] : 1.f, b3 = gn ? gsh[32 + 3] : 0.f;
 
-  float* at = smem;                                  // [(h1-h0) x W] updated alpha
-  float* post = smem + (size_t)(a.band + 2) * W;     // [(r1-r0) x W] post-update alive mask
-  const int na = (h1 - h0) * W;
-  for (int e = tid; e < na; e += kThreads) {
-    const size_t p = 3 * HW + (size_t)h0 * W + e;
-    float d = db[p];
+  // (3) updated alpha over band + halo, then the post-update alive mask (3x3 max-pool, -inf pad)
+  auto alpha_at = [&](float xa, float d) {
     if (gn) d = (d - mu) * rs * g3 + b3;
-    at[e] = xb[p] + tanhf(d) * a.gain;
+    return xa + tanhf(d) * a.gain;
+  };
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int e = tid + u * kThreads;
+    if (e < na) at[e] = alpha_at(ax[u], ad[u]);
+  }
+  for (int e = tid + NA * kThreads; e < na; e += kThreads) {
+    const size_t p = 3 * HW + (size_t)h0 * W + e;
+    at[e] = alpha_at(xb[p], db[p]);
   }
   __syncthreads();
-  const int nb = (r1 - r0) * W;
   for (int e = tid; e < nb; e += kThreads) {
     const int i = r0 + e / W, j = e - (e / W) * W;
     float mx = -INFINITY;
@@ -867,60 +940,34 @@ __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
   }
   __syncthreads();
 
-  const size_t base = (size_t)r0 * W;
-  if ((W & 3) == 0) {
-    // a thread owns a 4-cell quad and walks the channels; four channels' loads are issued
-    // together (memory-level parallelism) before their tanh/residual math
-    const int nq = nb >> 2;
-    for (int q = tid; q < nq; q += kThreads) {
-      const size_t cell = base + 4 * (size_t)q;
-      {
-        const f4 al = *reinterpret_cast<const f4*>(at + (r0 - h0) * W + 4 * q);
-        const f4 ps = *reinterpret_cast<const f4*>(post + 4 * q);
-        *reinterpret_cast<f4*>(ob + 3 * HW + cell) = al * ps;
-      }
-      for (int c0 = 0; c0 < C; c0 += 4) {
-        f4 xv[4], dv[4];
+  // (4) main pass: out = x + tanh(GN(dx))*gain; alpha channel = x~_3 * post
+  auto store_items = [&](int it0) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int c = c0 + u;
-          if (c < C && c != 3) {
-            xv[u] = *reinterpret_cast<const f4*>(xb + c * HW + cell);
-            dv[u] = *reinterpret_cast<const f4*>(db + c * HW + cell);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int c = c0 + u;
-          if (c >= C || c == 3) continue;
-          f4 d = dv[u];
-          if (gn) {
-            const float gc = a.gamma[c] * rs, bc = a.beta[c];
-            d = (d - mu) * gc + bc;
-          }
-          f4 v;
-          v[0] = xv[u][0] + tanhf(d[0]) * a.gain;
-          v[1] = xv[u][1] + tanhf(d[1]) * a.gain;
-          v[2] = xv[u][2] + tanhf(d[2]) * a.gain;
-          v[3] = xv[u][3] + tanhf(d[3]) * a.gain;
-          *reinterpret_cast<f4*>(ob + c * HW + cell) = v;
-        }
-      }
-    }
-  } else {
-    for (int it = tid; it < C * nb; it += kThreads) {
-      const int c = it / nb, e = it - c * nb;
-      const size_t p = c * HW + base + e;
-      float v;
+    for (int u = 0; u < KU; ++u) {
+      const int it = it0 + u * kThreads;
+      if (it >= nitems) continue;
+      const int c = it / nv, q = it - c * nv;
+      const size_t p = (size_t)c * HW + base + (size_t)V * q;
+      vf v;
       if (c == 3) {
-        v = at[(r0 - h0) * W + e] * post[e];
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = at[(r0 - h0) * W + V * q + k] * post[V * q + k];
       } else {
-        float d = db[p];
-        if (gn) d = (d - mu) * (a.gamma[c] * rs) + a.beta[c];
-        v = xb[p] + tanhf(d) * a.gain;
+        const float gc = gn ? gsh[c] * rs : 1.f, bc = gn ? gsh[32 + c] : 0.f;
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          float d = dv[u][k];
+          if (gn) d = (d - mu) * gc + bc;
+          v[k] = xv[u][k] + tanhf(d) * a.gain;
+        }
       }
-      ob[p] = v;
+      *reinterpret_cast<vf*>(ob + p) = v;
     }
+  };
+  store_items(tid);
+  for (int it0 = tid + KU * kThreads; it0 < nitems; it0 += KU * kThreads) {
+    load_items(it0);
+    store_items(it0);
   }
   if (a.attn) {
     const float amn = sh_norm[2], amx = sh_norm[3];
@@ -929,6 +976,27 @@ __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
       *q = (*q - amn) / (amx - amn + 1e-8f);
     }
   }
+}
+
+__global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float sh_norm[4 + 64];
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x / a.nbands, band = blockIdx.x - b * a.nbands;
+  if (a.active && !a.active[b]) {   // masked step: an inactive sample passes through unchanged
+    const size_t HW = (size_t)a.H * a.W;
+    const int r0 = band * a.band, r1 = min(a.H, r0 + a.band);
+    const float* xs_ = a.x + (size_t)b * a.C * HW;
+    float* os_ = a.out + (size_t)b * a.C * HW;
+    const int nbc = (r1 - r0) * a.W;
+    for (int it = tid; it < a.C * nbc; it += kThreads) {
+      const int c = it / nbc, e = it - c * nbc;
+      os_[(size_t)c * HW + (size_t)r0 * a.W + e] = xs_[(size_t)c * HW + (size_t)r0 * a.W + e];
+    }
+    return;
+  }
+  if ((a.W & 3) == 0) k2_body<4>(a, smem, sh_norm);
+  else k2_body<1>(a, smem, sh_norm);
 }
 
 // normalise a message-only attention map (no K2 in message mode)
@@ -1091,7 +1159,9 @@ static const Variant kVariants[] = {
     GNCA_FV(16, 128, 36, 24, 4, 4, 8, 512),
     GNCA_FV(16, 128, 24, 24, 4, 4, 8, 512),
     GNCA_FV(16, 128, 8, 24, 4, 4, 8, 256),    // same, 8x24 tiles, 2 WGs / CU
+    GNCA_FV(16, 128, 8, 24, 4, 4, 8, 512),    // small batches: 8 waves per 8x24 tile (<= 1 group each)
     GNCA_FV(16, 128, 8, 24, 1, 1, 0, 256),    // classic NCA (no gather)
+    GNCA_FV(16, 128, 8, 24, 1, 1, 0, 512),
     // runtime geometry: every other shape class
     GNCA_GV(4, 32),   GNCA_GV(4, 64),   GNCA_GV(4, 128),  GNCA_GV(8, 32),   GNCA_GV(8, 64),
     GNCA_GV(8, 128),  GNCA_GV(12, 64),  GNCA_GV(12, 128), GNCA_GV(16, 32),  GNCA_GV(16, 64),
@@ -1176,7 +1246,10 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
       fixed_pick = &v;
       fixed_tiles = tiles;
       if (tiles >= fill) break;   // large batch: first (preferred) eligible variant
-    } else if (tiles > fixed_tiles) {
+    } else if (tiles > fixed_tiles ||
+               // same tile count and every tile gets a CU of its own: the wider workgroup
+               // (fewer 16-cell groups per wave: a shorter tile latency)
+               (tiles == fixed_tiles && tiles <= device_cus() && v.NT > fixed_pick->NT)) {
       fixed_pick = &v;
       fixed_tiles = tiles;
     }

@@ -17,8 +17,13 @@ VARIANTS = {
     "no_planes": 32, "mfma_only": 1 | 2 | 4 | 16 | 32, "no_mfma_no_store": 8 | 16,
     "stage_only": 2 | 4 | 8 | 16 | 32,
     "no_fire": 64, "no_zero": 128, "no_reduce": 256,
+    "no_tiles": 512, "no_tiles_no_fill": 512 | 1024,
     "bare": 2 | 4 | 8 | 16 | 32 | 64 | 128 | 256, "bare_no_stage": 1 | 2 | 4 | 8 | 16 | 32 | 64 | 128 | 256,
 }
+
+
+ONLY = [v for v in os.environ.get("ABLATE_ONLY", "").split(",") if v]   # e.g. "full,prof"
+CONFIG = os.environ.get("ABLATE_CONFIG", "headline")                    # a bench.py WORKLOADS key
 
 
 def build():
@@ -26,6 +31,8 @@ def build():
     src = os.path.join(ROOT, "graph_neural_cellular_automata_amd", "csrc", "gnca_step.hip")
     procs = []
     for name, bits in list(VARIANTS.items()) + [("prof", None)]:
+        if ONLY and name not in ONLY:
+            continue
         flags = ["-DGNCA_PROFILE"] if bits is None else [f"-DGNCA_ABLATE={bits}"]
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                *flags, f"-I{ROOT}/include", src, "-o", os.path.join(OUT, f"lib_{name}.so")]
@@ -44,6 +51,8 @@ def run(reps=15, rounds=3):
     dev = torch.device("cuda:0")
     libs = {}
     for name in VARIANTS:
+        if ONLY and name not in ONLY:
+            continue
         lib = ctypes.CDLL(os.path.join(OUT, f"lib_{name}.so"))
         lib.gnca_step_phases_f32.restype = ctypes.c_int
         lib.gnca_step_phases_f32.argtypes = [ctypes.POINTER(L.StepDesc), ctypes.POINTER(L.Weights)] + \
@@ -51,15 +60,16 @@ def run(reps=15, rounds=3):
         lib.gnca_workspace_bytes.restype = ctypes.c_size_t
         lib.gnca_workspace_bytes.argtypes = [ctypes.POINTER(L.StepDesc)]
         libs[name] = lib
-    B, H = 1024, 72
-    wl = bench.WORKLOADS["headline"]
+    wl = bench.WORKLOADS[CONFIG]
+    B, H = wl["B"], wl["H"]
     w, keep = bench.weight_struct(bench.load_weights(dev, wl), wl)
-    x = torch.rand(B, 16, H, H, device=dev)
+    x = torch.rand(B, wl["C"], H, H, device=dev)
     out = torch.empty_like(x)
     from graph_neural_cellular_automata_amd.modules.graph_augmentation import GraphAugmentation
     build_offsets = GraphAugmentation._build_offsets
-    d = bench.make_desc(wl, B, H, H, random.Random(0).sample(build_offsets(4), 8), 0)
-    ws = torch.empty(libs["full"].gnca_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
+    offs = random.Random(0).sample(build_offsets(wl["R"]), wl["K"]) if wl["graph"] else []
+    d = bench.make_desc(wl, B, H, H, offs, 0)
+    ws = torch.empty(next(iter(libs.values())).gnca_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream()
     res = {n: [] for n in libs}
     for _ in range(rounds):
@@ -80,7 +90,7 @@ def run(reps=15, rounds=3):
     # phase timers of the profile build (s_memtime cycles summed over each workgroup's tiles)
     pl = ctypes.CDLL(os.path.join(OUT, "lib_prof.so"))
     pl.gnca_step_phases_f32.restype = ctypes.c_int
-    pl.gnca_step_phases_f32.argtypes = libs["full"].gnca_step_phases_f32.argtypes
+    pl.gnca_step_phases_f32.argtypes = next(iter(libs.values())).gnca_step_phases_f32.argtypes
     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
     e0.record(st)
     assert pl.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), x.data_ptr(), out.data_ptr(), None,
