@@ -65,7 +65,7 @@ __device__ float g_zero[4];  // LDS-DMA source for off-image cells (zero-initial
 // workgroup accumulates s_memtime deltas per phase; gnca_prof_dump copies them out.
 #ifdef GNCA_PROFILE
 constexpr int kProfPhases = 8;
-__device__ unsigned long long g_prof[1024][kProfPhases];
+__device__ unsigned long long g_prof[1024][2 * kProfPhases];   // [.][8..15]: spare (role profiles)
 #define PROF_DECL unsigned long long prof_t = __builtin_amdgcn_s_memtime(), prof_acc[kProfPhases] = {0};
 #define PROF_MARK(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
 #define PROF_STORE do { if (threadIdx.x == 0) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][i_] = prof_acc[i_]; } while (0)

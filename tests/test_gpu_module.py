@@ -182,3 +182,43 @@ def test_fire_mask_u8_matches_oracle_hash(dev):
     m = S.fire_mask(d, dev).cpu().numpy()
     ref = O.hash_fire_mask(123456789, 17, 1000, 3, 20, 33, 0.37)
     np.testing.assert_array_equal(m.astype(np.float32), ref)
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_large_batch_path_vs_oracle(dev, graph):
+    """B=256 x 16 x 72 x 72 (the large-batch fixed-geometry K1, 24x36 tiles): three samples of one
+    step against the float64 oracle, and a shard split is bitwise equal."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    m = _trained_like(dev, seed=3)
+    B = 256
+    x = _state(B, 16, 72, 72, dev, seed=9)
+    random.seed(4)
+    offs = random.sample(m.graph.offsets, 8) if graph else []
+    tensors = dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
+                   b1=m.update_net[0].bias, w2=m.update_net[2].weight, gn_weight=m.norm.weight,
+                   gn_bias=m.norm.bias)
+    if graph:
+        tensors.update(m.graph.weight_tensors())
+    w, keep = S.make_weights(tensors)
+    flags = L.USE_GROUPNORM | ((L.GRAPH | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE) if graph else 0)
+
+    def desc(Bn, base):
+        return S.make_desc(B=Bn, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs, flags=flags,
+                           update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                           fire_mode=L.FIRE_HASH, rng_seed=42, rng_step=3, sample_base=base)
+
+    out, _ = S.step(desc(B, 0), w, x)
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    cfg = dict(update_gain=0.05, alpha_thr=0.12, use_groupnorm=True, graph=graph,
+               message_gain=0.25, hidden_only=True, zero_padded_shift=False, alive_to_alive=True)
+    fm = O.hash_fire_mask(42, 3, 0, B, 72, 72, 0.5)
+    for i in (0, 131, 255):
+        ref = O.nca_step(x[i:i + 1].cpu().numpy().astype(np.float64), p, cfg, chosen=offs,
+                         fire_mask=fm[i:i + 1])
+        np.testing.assert_allclose(out[i:i + 1].cpu().numpy(), ref, rtol=1e-5, atol=2e-6)
+    # shard invariance
+    lo, _ = S.step(desc(240, 0), w, x[:240].contiguous())
+    hi, _ = S.step(desc(16, 240), w, x[240:].contiguous())   # small shard: the small-batch variant
+    assert torch.equal(out[:240], lo)
+    np.testing.assert_allclose(out[240:].cpu().numpy(), hi.cpu().numpy(), rtol=1e-5, atol=2e-6)

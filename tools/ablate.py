@@ -97,16 +97,26 @@ def run(reps=15, rounds=3):
                                    None, ws.data_ptr(), ws.numel(), st.cuda_stream, 2) == 0
     e1.record(st)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * (1024 * 8))()
+    buf = (ctypes.c_ulonglong * (1024 * 16))()
     assert pl.gnca_prof_dump(buf) == 0
     import numpy as np
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8).astype(np.float64)
-    a = a[a.sum(1) > 0]
-    names = ["dma_issue", "fire+dma_wait", "planes", "compaction", "groups", "reduction", "-", "loop_tail"]
-    tot = a.sum(1).mean()
-    print(f"prof build: {e0.elapsed_time(e1):.3f} ms; mean cycles per workgroup {tot:.0f} over {len(a)} WGs")
-    for i, nm in enumerate(names):
-        print(f"  {nm:14s} {a[:, i].mean():12.0f} cycles  {100 * a[:, i].mean() / tot:5.1f} %")
+    full = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16).astype(np.float64)
+    ws = full[:, 8:].sum() > 0
+    if ws:
+        sets = [("producer wave 0", ["dma_issue", "fire+dma_wait+pbar", "planes+pbar", "compaction",
+                                     "y_compute", "wait_empty", "end_tile_pbar", "end_stream"], full[:, :8]),
+                ("consumer wave 4", ["wait_full", "compute", "read+flush", "-", "-", "-", "-", "-"], full[:, 8:])]
+    else:
+        sets = [("wave 0", ["dma_issue", "fire+dma_wait", "planes", "compaction", "groups", "reduction",
+                            "-", "loop_tail"], full[:, :8])]
+    print(f"prof build: {e0.elapsed_time(e1):.3f} ms")
+    for title, names, a in sets:
+        a = a[a.sum(1) > 0]
+        tot = a.sum(1).mean()
+        print(f" {title}: mean cycles per workgroup {tot:.0f} over {len(a)} WGs")
+        for i, nm in enumerate(names):
+            if nm != "-":
+                print(f"  {nm:20s} {a[:, i].mean():12.0f} cycles  {100 * a[:, i].mean() / tot:5.1f} %")
 
 
 if __name__ == "__main__":
