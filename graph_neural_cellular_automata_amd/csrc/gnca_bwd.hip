@@ -90,16 +90,6 @@ __device__ __forceinline__ double2 block_sum2(double a, double b, double* red) {
   return make_double2(ta, tb);
 }
 
-__device__ __forceinline__ void sample_stats(const double* stats, int b, int tps, double n, float eps,
-                                             float* mu, float* rs) {
-  double t1, t2;  // the forward K2's fixed-order sum (same values bit for bit)
-  seq_sum2(stats + (size_t)b * tps * 2, tps, 2, &t1, &t2);
-  const double m = t1 / n;
-  double var = t2 / n - m * m;
-  if (var < 0.0) var = 0.0;
-  *mu = (float)m;
-  *rs = (float)(1.0 / sqrt(var + (double)eps));
-}
 
 // ------------------------------------------------------------------------------------------
 // BA: gate / tanh / GroupNorm backward prep (ncagraph.py:153-166)
@@ -142,14 +132,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_gnprep(const BAArgs a) {
     if (tid < 2 + 2 * C) a.part[(size_t)blockIdx.x * (2 + 2 * C) + tid] = 0.0;
     return;
   }
-  if (tid == 0) {
-    float mu = 0.f, rs = 1.f;
-    if (gn) sample_stats(a.stats, b, a.tps, (double)C * (double)HW, a.eps, &mu, &rs);
-    sh[0] = mu;
-    sh[1] = rs;
-  }
-  __syncthreads();
-  const float mu = sh[0], rs = sh[1];
+  const int lane = tid & 63, wave = tid >> 6;
   const float* xb = a.x + (size_t)b * C * HW;
   const float* db = a.dx + (size_t)b * C * HW;
   const float* gb = a.gy + (size_t)b * C * HW;
@@ -157,18 +140,75 @@ __global__ __launch_bounds__(kThreads) void gnca_b_gnprep(const BAArgs a) {
   float* ub = a.U + (size_t)b * C * HW;
   float* at = smem;                                  // updated alpha, band rows + halo
   float* post = smem + (size_t)(a.band + 2) * W;     // post-update alive mask of the band
-  {
-    const float g3 = gn ? a.gamma[3] : 1.f, b3 = gn ? a.beta[3] : 0.f;
-    const int na = (h1 - h0) * W;
-    for (int e = tid; e < na; e += kThreads) {
+  const int na = (h1 - h0) * W, nb = (r1 - r0) * W;
+  const size_t base = (size_t)r0 * W;
+  // Latency first: the alpha rows and this wave's first channel block are loaded before the
+  // per-sample statistics are known (one memory latency for the prologue of a small band).
+  constexpr int NA = 2;
+  float ax[NA], ad[NA];
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int e = tid + u * kThreads;
+    if (e < na) {
       const size_t p = 3 * HW + (size_t)h0 * W + e;
-      float d = db[p];
-      if (gn) d = (d - mu) * rs * g3 + b3;   // the forward K2's expression for alpha
-      at[e] = xb[p] + tanhf(d) * a.gain;
+      ax[u] = xb[p];
+      ad[u] = db[p];
+    }
+  }
+  // one wave per channel (c = cb + wave + NW*j), JM channels of the wave in flight at once
+  constexpr int JM = 4;
+  float dv[JM][4], gv[JM][4];
+  auto load_block = [&](int cb, int e0) {
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      const int c = cb + wave + NW * j;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 64 * u + lane;
+        const size_t p = (size_t)c * HW + base + e;
+        const bool ok = c < C && e < nb;
+        dv[j][u] = ok ? db[p] : 0.f;
+        gv[j][u] = ok ? gb[p] : 0.f;
+      }
+    }
+  };
+  load_block(0, 0);
+  if (wave == 0) {
+    float mu = 0.f, rs = 1.f;
+    if (gn) {
+      double t1, t2;   // the forward K2's fixed-order sum (same values bit for bit)
+      wave_seq_sum2(a.stats + (size_t)b * a.tps * 2, a.tps, &t1, &t2);
+      const double n = (double)C * (double)HW;
+      const double m = t1 / n;
+      double var = t2 / n - m * m;
+      if (var < 0.0) var = 0.0;
+      mu = (float)m;
+      rs = (float)(1.0 / sqrt(var + (double)a.eps));
+    }
+    if (lane == 0) {
+      sh[0] = mu;
+      sh[1] = rs;
     }
   }
   __syncthreads();
-  const int nb = (r1 - r0) * W;
+  const float mu = sh[0], rs = sh[1];
+  {
+    const float g3 = gn ? a.gamma[3] : 1.f, b3 = gn ? a.beta[3] : 0.f;
+    auto alpha_at = [&](float xa, float d) {
+      if (gn) d = (d - mu) * rs * g3 + b3;   // the forward K2's expression for alpha
+      return xa + tanhf(d) * a.gain;
+    };
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int e = tid + u * kThreads;
+      if (e < na) at[e] = alpha_at(ax[u], ad[u]);
+    }
+    for (int e = tid + NA * kThreads; e < na; e += kThreads) {
+      const size_t p = 3 * HW + (size_t)h0 * W + e;
+      at[e] = alpha_at(xb[p], db[p]);
+    }
+  }
+  __syncthreads();
   for (int e = tid; e < nb; e += kThreads) {
     const int i = r0 + e / W, j = e - (e / W) * W;
     float mx = -INFINITY;
@@ -181,54 +221,56 @@ __global__ __launch_bounds__(kThreads) void gnca_b_gnprep(const BAArgs a) {
     post[e] = mx > a.thr ? 1.f : 0.f;
   }
   __syncthreads();
-  // one wave per channel (c = wave, wave + NW, ...): wave-level reductions need no barrier, and
-  // 4 cells per lane are loaded together, so a small band is not a chain of 2C block reductions
-  const size_t base = (size_t)r0 * W;
-  const int lane = tid & 63, wave = tid >> 6;
   double su = 0.0, sux = 0.0;
   double* outp = a.part + (size_t)blockIdx.x * (2 + 2 * C);
-  for (int c = wave; c < C; c += NW) {
-    const float gc = gn ? a.gamma[c] : 1.f, bc = gn ? a.beta[c] : 0.f;
-    const float gcr = gc * rs;
-    double sg = 0.0, sgx = 0.0;
-    for (int e0 = 0; e0 < nb; e0 += 4 * 64) {
-      float dv[4], gv[4];
+  for (int cb = 0; cb < C; cb += NW * JM) {
+  double sg[JM], sgx[JM];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = e0 + 64 * u + lane;
-        const size_t p = (size_t)c * HW + base + e;
-        dv[u] = e < nb ? db[p] : 0.f;
-        gv[u] = e < nb ? gb[p] : 0.f;
-      }
+  for (int j = 0; j < JM; ++j) { sg[j] = 0.0; sgx[j] = 0.0; }
+  for (int e0 = 0; e0 < nb; e0 += 4 * 64) {
+    if (e0 > 0 || cb > 0) load_block(cb, e0);
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      const int c = cb + wave + NW * j;
+      if (c >= C) continue;
+      const float gc = gn ? a.gamma[c] : 1.f, bc = gn ? a.beta[c] : 0.f;
+      const float gcr = gc * rs;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int e = e0 + 64 * u + lane;
         if (e >= nb) continue;
         const size_t p = (size_t)c * HW + base + e;
-        const float d = dv[u];
+        const float d = dv[j][u];
         const float xhat = (d - mu) * rs;
         const float xn = gn ? (c == 3 ? (d - mu) * rs * gc + bc : (d - mu) * gcr + bc) : d;
         const float t = tanhf(xn);
-        float g = gv[u];
+        float g = gv[j][u];
         if (c == 3) g *= post[e];                       // x * gate, gate on alpha only (:158-166)
         gxb[p] = g;                                     // the residual x + ... (:155)
         const float gxn = g * a.gain * (1.f - t * t);   // tanh(.)*update_gain (:154)
         const float uu = gn ? gxn * gc : gxn;
         ub[p] = uu;
-        sg += (double)gxn;
-        sgx += (double)gxn * (double)xhat;
+        sg[j] += (double)gxn;
+        sgx[j] += (double)gxn * (double)xhat;
         su += (double)uu;
         sux += (double)uu * (double)xhat;
       }
     }
+  }
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int c = cb + wave + NW * j;
+    if (c >= C) continue;
+    double x1 = sg[j], x2 = sgx[j];
     for (int off = 32; off > 0; off >>= 1) {
-      sg += __shfl_xor(sg, off);
-      sgx += __shfl_xor(sgx, off);
+      x1 += __shfl_xor(x1, off);
+      x2 += __shfl_xor(x2, off);
     }
     if (lane == 0) {
-      outp[2 + 2 * c] = sgx;
-      outp[3 + 2 * c] = sg;
+      outp[2 + 2 * c] = x2;
+      outp[3 + 2 * c] = x1;
     }
+  }
   }
   const double2 r = block_sum2(su, sux, red);
   if (tid == 0) {
@@ -238,24 +280,32 @@ __global__ __launch_bounds__(kThreads) void gnca_b_gnprep(const BAArgs a) {
 }
 
 // BS: per-sample GroupNorm-backward coefficients (mu, rstd, mean U, mean U*xhat)
-__global__ __launch_bounds__(kThreads) void gnca_b_coef(const double* stats, const double* part,
-                                                        float* coef, int B, int C, int HW, int tps,
-                                                        int nbands, float eps, int use_gn) {
-  const int b = blockIdx.x * kThreads + threadIdx.x;
-  if (b >= B) return;
+// one wave per sample: both partial lists load in one memory latency (wave_seq_sum2 keeps
+// seq_sum2's order, so mean / rstd are the forward K2's bit for bit)
+__global__ __launch_bounds__(64) void gnca_b_coef(const double* stats, const double* part,
+                                                  float* coef, int B, int C, int HW, int tps,
+                                                  int nbands, float eps, int use_gn) {
+  const int b = blockIdx.x;
   float mu = 0.f, rs = 1.f, mu_u = 0.f, mu_ux = 0.f;
   if (use_gn) {
     const double n = (double)C * (double)HW;
-    sample_stats(stats, b, tps, n, eps, &mu, &rs);
-    double su, sux;
-    seq_sum2(part + (size_t)b * nbands * (2 + 2 * C), nbands, 2 + 2 * C, &su, &sux);
+    double t1, t2, su, sux;
+    wave_seq_sum2(stats + (size_t)b * tps * 2, tps, &t1, &t2);
+    wave_seq_sum2(part + (size_t)b * nbands * (2 + 2 * C), nbands, &su, &sux, 2 + 2 * C);
+    const double m = t1 / n;
+    double var = t2 / n - m * m;
+    if (var < 0.0) var = 0.0;
+    mu = (float)m;
+    rs = (float)(1.0 / sqrt(var + (double)eps));
     mu_u = (float)(su / n);
     mu_ux = (float)(sux / n);
   }
-  coef[4 * b + 0] = mu;
-  coef[4 * b + 1] = rs;
-  coef[4 * b + 2] = mu_u;
-  coef[4 * b + 3] = mu_ux;
+  if (threadIdx.x == 0) {
+    coef[4 * b + 0] = mu;
+    coef[4 * b + 1] = rs;
+    coef[4 * b + 2] = mu_u;
+    coef[4 * b + 3] = mu_ux;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -376,31 +426,52 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     const int f = slot / CP, c = slot - f * CP;
     return (hid < Hd && slot < 3 * CP && c < C) ? a.w1[(size_t)hid * 3 * C + f * C + c] : 0.f;
   };
-  lds_fill<kThreads, 8>(w1f, MT * 64 * KSP, tid, [&](int idx) {   // A[hid][slot], k-step s
-    const int s = idx % KSP, ml = idx / KSP, l = ml & 63, m = ml >> 6;
-    return s < KS ? w1at(h0 + 16 * m + (l & 15), 4 * s + (l >> 4)) : 0.f;
-  });
-  lds_fill<kThreads, 8>(w1t, FT * 64 * S1T, tid, [&](int idx) {   // A[slot][hid], k-step (m, r)
-    const int e = idx % S1T, fl = idx / S1T, l = fl & 63, ft = fl >> 6;
-    const int m = e >> 2, r = e & 3;
-    return e < 4 * MT ? w1at(h0 + 16 * m + 4 * (l >> 4) + r, 16 * ft + (l & 15)) : 0.f;
-  });
-  lds_fill<kThreads, 8>(w2t, MT * 64 * S2T, tid, [&](int idx) {   // A[hid][c], k-step (mo, s)
-    const int e = idx % S2T, ml = idx / S2T, l = ml & 63, m = ml >> 6;
-    const int mo = e >> 2, s4 = e & 3;
-    const int c = 16 * mo + 4 * (l >> 4) + s4, hid = h0 + 16 * m + (l & 15);
-    return (e < 4 * MO && c < C && hid < Hd) ? a.w2[(size_t)c * Hd + hid] : 0.f;
-  });
-  lds_fill<kThreads, 4>(wms, 16 * MO * SWM, tid, [&](int idx) {
-    const int co = idx / SWM, ci = idx - co * SWM;
-    return (msg && co < C && ci < C) ? a.wm[co * C + ci] : 0.f;
-  });
-  lds_fill<kThreads, 1>(b1s, HB, tid, [&](int idx) { return h0 + idx < Hd ? a.b1[h0 + idx] : 0.f; });
-  lds_fill<kThreads, 1>(bms, 16 * MO, tid, [&](int idx) { return (msg && idx < C) ? a.bm[idx] : 0.f; });
-  lds_fill<kThreads, 4>(percs, CP * 36, tid, [&](int idx) {
-    const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
-    return (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
-  });
+  // every load of the slice's weight set in flight before the first LDS store (one memory
+  // latency for the prologue: most of a small-batch launch)
+  {
+    constexpr int cKSP = odd4(3 * CP / 4), cS1T = odd4(4 * MT), cS2T = odd4(4 * MO);
+    constexpr int cSWM = odd4(16 * MO);
+    RegFill<kThreads, MT * 64 * cKSP> f1;
+    RegFill<kThreads, FT * 64 * cS1T> f2;
+    RegFill<kThreads, MT * 64 * cS2T> f3;
+    RegFill<kThreads, 16 * MO * cSWM> f4_;
+    RegFill<kThreads, HB> f5;
+    RegFill<kThreads, 16 * MO> f6;
+    RegFill<kThreads, CP * 36> f7;
+    f1.load(tid, [&](int idx) {   // A[hid][slot], k-step s
+      const int s = idx % cKSP, ml = idx / cKSP, l = ml & 63, m = ml >> 6;
+      return s < KS ? w1at(h0 + 16 * m + (l & 15), 4 * s + (l >> 4)) : 0.f;
+    });
+    f2.load(tid, [&](int idx) {   // A[slot][hid], k-step (m, r)
+      const int e = idx % cS1T, fl = idx / cS1T, l = fl & 63, ft = fl >> 6;
+      const int m = e >> 2, r = e & 3;
+      return e < 4 * MT ? w1at(h0 + 16 * m + 4 * (l >> 4) + r, 16 * ft + (l & 15)) : 0.f;
+    });
+    f3.load(tid, [&](int idx) {   // A[hid][c], k-step (mo, s)
+      const int e = idx % cS2T, ml = idx / cS2T, l = ml & 63, m = ml >> 6;
+      const int mo = e >> 2, s4 = e & 3;
+      const int c = 16 * mo + 4 * (l >> 4) + s4, hid = h0 + 16 * m + (l & 15);
+      return (e < 4 * MO && c < C && hid < Hd) ? a.w2[(size_t)c * Hd + hid] : 0.f;
+    });
+    f4_.load(tid, [&](int idx) {
+      const int co = idx / cSWM, ci = idx - co * cSWM;
+      return (msg && co < C && ci < C) ? a.wm[co * C + ci] : 0.f;
+    });
+    f5.load(tid, [&](int idx) { return h0 + idx < Hd ? a.b1[h0 + idx] : 0.f; });
+    f6.load(tid, [&](int idx) { return (msg && idx < C) ? a.bm[idx] : 0.f; });
+    f7.load(tid, [&](int idx) {
+      const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
+      return (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
+    });
+    f1.store(w1f, tid);
+    f2.store(w1t, tid);
+    f3.store(w2t, tid);
+    f4_.store(wms, tid);
+    f5.store(b1s, tid);
+    f6.store(bms, tid);
+    f7.store(percs, tid);
+    static_assert(cKSP > 0 && cS1T > 0 && cS2T > 0 && cSWM > 0, "");
+  }
   __syncthreads();
   bool sobel;
   {
@@ -876,7 +947,9 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     BPROF_MARK(4);   // group loop
   }
 
-  // ---- this wave's partial gradients -> its own row (reduced later in a fixed order) ----
+  // ---- this wave's partial gradients -> its own row (reduced later in a fixed order).  (An LDS
+  //      combine of the 4 waves into one row per workgroup measured slower: 131 vs 106 us per
+  //      B=16 40x40 backward.) ----
   float* outp = a.part + ((size_t)blockIdx.x * NW + wave) * a.npart;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -978,26 +1051,6 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   float* wts = as_ + TH * TW;                          // [k]
   float* pws = wts + (k > 0 ? k : 1);                  // [C*27] perception weights
   const float* xb = a.x + (size_t)b * C * HW;
-  lds_fill<kThreads, 2>(pws, C * 27, tid, [&](int e) { return a.perc[e]; });
-  if (msg) {
-    for (int o = tid; o < k; o += kThreads) wts[o] = a.offw ? a.offw[(size_t)b * k + o] : a.uniform_w;
-    for (int n = tid; n < TH * TW; n += kThreads) {
-      const int i = i0 + n / TW, j = j0 + n % TW;
-      float v9[9];   // the 3x3 alpha neighbourhood, all nine loads in flight
-#pragma unroll
-      for (int u = 0; u < 3; ++u)
-#pragma unroll
-        for (int v = 0; v < 3; ++v) {
-          const int ii = i + u - 1, jj = j + v - 1;
-          v9[3 * u + v] = (i < H && j < W && ii >= 0 && ii < H && jj >= 0 && jj < W)
-                              ? xb[3 * HW + (size_t)ii * W + jj] : -INFINITY;
-        }
-      float mx = v9[0];
-#pragma unroll
-      for (int t = 1; t < 9; ++t) mx = fmaxf(mx, v9[t]);
-      as_[n] = a2a ? (mx > a.graph_alpha_thr ? 1.f : 0.f) : 1.f;
-    }
-  }
   // per-thread staging plan: element e = tid + 256*i of [3 dY planes | dG halo]; source offset
   // within the channel plane (or -1 = zero), and the plane group (0..2 dY, 3 dG)
   int soff[kBCStage];
@@ -1052,8 +1105,30 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
       dst[u] = (n < TH * TW && i < H && j < W) ? a.gx[((size_t)b * C + c) * HW + (size_t)i * W + j] : 0.f;
     }
   };
+  // the first channel's staging loads go out before the perception weights / sender mask, so
+  // the prologue waits out one memory latency, not three
   load(c_lo);
   load_gx(c_lo, gxc);
+  lds_fill<kThreads, 2>(pws, C * 27, tid, [&](int e) { return a.perc[e]; });
+  if (msg) {
+    for (int o = tid; o < k; o += kThreads) wts[o] = a.offw ? a.offw[(size_t)b * k + o] : a.uniform_w;
+    for (int n = tid; n < TH * TW; n += kThreads) {
+      const int i = i0 + n / TW, j = j0 + n % TW;
+      float v9[9];   // the 3x3 alpha neighbourhood, all nine loads in flight
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          const int ii = i + u - 1, jj = j + v - 1;
+          v9[3 * u + v] = (i < H && j < W && ii >= 0 && ii < H && jj >= 0 && jj < W)
+                              ? xb[3 * HW + (size_t)ii * W + jj] : -INFINITY;
+        }
+      float mx = v9[0];
+#pragma unroll
+      for (int t = 1; t < 9; ++t) mx = fmaxf(mx, v9[t]);
+      as_[n] = a2a ? (mx > a.graph_alpha_thr ? 1.f : 0.f) : 1.f;
+    }
+  }
   store(buf0);
   __syncthreads();
   for (int c = c_lo; c < c_hi; ++c) {
@@ -1626,7 +1701,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     if ((rc = bwd_check()) != GNCA_OK) return rc;
   }
   // BS
-  hipLaunchKernelGGL(gnca_b_coef, dim3((B + kThreads - 1) / kThreads), dim3(kThreads), 0, st, stats,
+  hipLaunchKernelGGL(gnca_b_coef, dim3(B), dim3(64), 0, st, stats,
                      (const double*)pa, coef, B, C, (int)HW, P.F.tps, P.nbands, d.gn_eps, P.gn ? 1 : 0);
   if ((rc = bwd_check()) != GNCA_OK) return rc;
   // BB, one launch per hidden slice

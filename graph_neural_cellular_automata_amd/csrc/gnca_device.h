@@ -46,9 +46,8 @@ __device__ __forceinline__ bool fire_at(int mode, const void* fire, float rate, 
 }
 
 __host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
-__host__ __device__ inline int odd4(int v) {  // round up to 4*odd: conflict-free 16-lane b128
-  v = r4(v);
-  return ((v >> 2) & 1) ? v : v + 4;
+__host__ __device__ constexpr int odd4(int v) {  // round up to 4*odd: conflict-free 16-lane b128
+  return ((((v + 3) & ~3) >> 2) & 1) ? ((v + 3) & ~3) : ((v + 3) & ~3) + 4;
 }
 
 // dst[idx] = f(idx) for idx < n (dst in LDS), U values per thread in flight: a plain strided loop
@@ -116,6 +115,35 @@ __device__ __forceinline__ void seq_sum2(const double* p, int n, int stride, dou
   }
   *s0 = a;
   *s1 = b;
+}
+
+// seq_sum2's sums (same order, same bits) computed by one whole wave: lane t loads pairs t,
+// t+64, ... (up to 256 pairs in one memory latency), then the pairs are added in index order
+// through lane broadcasts.  Every lane of the wave must call it; all get the sums.
+__device__ __forceinline__ void wave_seq_sum2(const double* p, int n, double* s0, double* s1,
+                                              int stride = 2) {
+  constexpr int PJ = 4;
+  if (n > 64 * PJ) {
+    seq_sum2(p, n, stride, s0, s1);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  double a[PJ], b[PJ];
+#pragma unroll
+  for (int j = 0; j < PJ; ++j) {
+    const int t = lane + 64 * j;
+    a[j] = t < n ? p[(size_t)stride * t] : 0.0;
+    b[j] = t < n ? p[(size_t)stride * t + 1] : 0.0;
+  }
+  double x = 0.0, y = 0.0;
+#pragma unroll
+  for (int j = 0; j < PJ; ++j)
+    for (int l = 0; l < 64 && 64 * j + l < n; ++l) {
+      x += __shfl(a[j], l);
+      y += __shfl(b[j], l);
+    }
+  *s0 = x;
+  *s1 = y;
 }
 
 // Where the forward keeps its intermediates in the step workspace (gnca_step.hip:make_plan);

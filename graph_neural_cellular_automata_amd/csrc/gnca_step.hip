@@ -1162,6 +1162,9 @@ static const Variant kVariants[] = {
     GNCA_FV(16, 128, 8, 24, 4, 4, 8, 512),    // small batches: 8 waves per 8x24 tile (<= 1 group each)
     GNCA_FV(16, 128, 8, 24, 1, 1, 0, 256),    // classic NCA (no gather)
     GNCA_FV(16, 128, 8, 24, 1, 1, 0, 512),
+    // the trainer's canvas (config.json img_size 40): 8x20 tiles, graph and no-message steps
+    GNCA_FV(16, 128, 8, 20, 4, 4, 8, 512),
+    GNCA_FV(16, 128, 8, 20, 1, 1, 0, 512),
     // runtime geometry: every other shape class
     GNCA_GV(4, 32),   GNCA_GV(4, 64),   GNCA_GV(4, 128),  GNCA_GV(8, 32),   GNCA_GV(8, 64),
     GNCA_GV(8, 128),  GNCA_GV(12, 64),  GNCA_GV(12, 128), GNCA_GV(16, 32),  GNCA_GV(16, 64),
@@ -1297,8 +1300,13 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // K2 bands: ~6 row bands per sample (many small workgroups: no wave-quantisation tail),
   // each with its alpha rows + 2 halo rows and its post mask in LDS (<= 48 KB)
   {
-    // ~6 bands per sample; more (thinner) bands when the batch is too small to fill the chip
-    const long nb_target = std::max<long>(6, (2L * device_cus() + d->B - 1) / d->B);
+    // bands of ~4 rows (measured on the B=1024 72^2 bench: 4 rows 0.177 ms, 12 rows 0.194 ms,
+    // 24 rows 0.209 ms per launch; tools/k2_band_sweep.sh); thinner when the batch is too small
+    // to fill the chip
+    // (narrow, 16-channel canvases; wide / 32-channel ones keep ~6 bands per sample: 128^2 x 32ch
+    // measured 0.164 ms at 22 rows, 0.184 ms at 4)
+    const bool thin = (long)d->W * d->C <= 96L * 16;
+    const long nb_target = std::max<long>(thin ? (d->H + 3) / 4 : 6, (2L * device_cus() + d->B - 1) / d->B);
     long rows = (d->H + nb_target - 1) / nb_target;
     static const char* band_env = getenv("GNCA_K2_BAND");   // measurement knob (A/B runs only)
     if (band_env && atoi(band_env) > 0) rows = atoi(band_env);
