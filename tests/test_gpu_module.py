@@ -222,3 +222,47 @@ def test_large_batch_path_vs_oracle(dev, graph):
     hi, _ = S.step(desc(16, 240), w, x[240:].contiguous())   # small shard: the small-batch variant
     assert torch.equal(out[:240], lo)
     np.testing.assert_allclose(out[240:].cpu().numpy(), hi.cpu().numpy(), rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("msg", [0.25, 0.0])
+def test_c32_two_phase_path_vs_oracle(dev, msg):
+    """BASELINE config 5's shape class (32 ch, 128 x 128, r = 5, K = 16) at B=64 takes the
+    two-channel-phase K1 (gnca_k1_2ph): two samples of one step against the float64 oracle
+    (message on, and message_gain 0 = the classic-style no-gather variant), and a shard split is
+    bitwise equal."""
+    from graph_neural_cellular_automata_amd import NeuralCAGraph
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    torch.manual_seed(5)
+    m = NeuralCAGraph(32, 128, update_gain=0.05, alpha_thr=0.12, message_gain=msg,
+                      graph_attention_radius=5, graph_num_neighbors=16,
+                      graph_zero_padded_shift=False).to(dev).eval()
+    with torch.no_grad():
+        m.update_net[2].weight.normal_(0, 0.02)
+    B, H = 64, 128
+    x = _state(B, 32, H, H, dev, seed=13)
+    random.seed(8)
+    offs = random.sample(m.graph.offsets, 16)
+    tensors = dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
+                   b1=m.update_net[0].bias, w2=m.update_net[2].weight, gn_weight=m.norm.weight,
+                   gn_bias=m.norm.bias, **m.graph.weight_tensors())
+    w, keep = S.make_weights(tensors)
+
+    def desc(Bn, base):
+        return S.make_desc(B=Bn, C=32, H=H, W=H, hidden=128, d_model=16, offsets=offs,
+                           flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                           update_gain=0.05, alpha_thr=0.12, message_gain=msg, fire_rate=0.5,
+                           fire_mode=L.FIRE_HASH, rng_seed=42, rng_step=1, sample_base=base)
+
+    out, _ = S.step(desc(B, 0), w, x)
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    cfg = dict(update_gain=0.05, alpha_thr=0.12, use_groupnorm=True, graph=True,
+               message_gain=msg, hidden_only=True, zero_padded_shift=False, alive_to_alive=True)
+    fm = O.hash_fire_mask(42, 1, 0, B, H, H, 0.5)
+    for i in (0, 63):
+        ref = O.nca_step(x[i:i + 1].cpu().numpy().astype(np.float64), p, cfg, chosen=offs,
+                         fire_mask=fm[i:i + 1])
+        np.testing.assert_allclose(out[i:i + 1].cpu().numpy(), ref, rtol=1e-5, atol=2e-6)
+    lo, _ = S.step(desc(32, 0), w, x[:32].contiguous())
+    hi, _ = S.step(desc(32, 32), w, x[32:].contiguous())
+    assert torch.equal(out, torch.cat([lo, hi]))
