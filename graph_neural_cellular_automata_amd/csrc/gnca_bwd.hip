@@ -176,8 +176,8 @@ __global__ __launch_bounds__(kThreads) void gnca_b_gnprep(const BAArgs a) {
   if (wave == 0) {
     float mu = 0.f, rs = 1.f;
     if (gn) {
-      double t1, t2;   // the forward K2's fixed-order sum (same values bit for bit)
-      wave_seq_sum2(a.stats + (size_t)b * a.tps * 2, a.tps, &t1, &t2);
+      double t1, t2;   // wave_sum2, as the forward K2: the same mean / rstd bit for bit
+      wave_sum2(a.stats + (size_t)b * a.tps * 2, a.tps, &t1, &t2);
       const double n = (double)C * (double)HW;
       const double m = t1 / n;
       double var = t2 / n - m * m;
@@ -280,8 +280,8 @@ __global__ __launch_bounds__(kThreads) void gnca_b_gnprep(const BAArgs a) {
 }
 
 // BS: per-sample GroupNorm-backward coefficients (mu, rstd, mean U, mean U*xhat)
-// one wave per sample: both partial lists load in one memory latency (wave_seq_sum2 keeps
-// seq_sum2's order, so mean / rstd are the forward K2's bit for bit)
+// one wave per sample: both partial lists load in one memory latency (wave_sum2, as the forward
+// K2, so mean / rstd are the forward's bit for bit)
 __global__ __launch_bounds__(64) void gnca_b_coef(const double* stats, const double* part,
                                                   float* coef, int B, int C, int HW, int tps,
                                                   int nbands, float eps, int use_gn) {
@@ -290,8 +290,8 @@ __global__ __launch_bounds__(64) void gnca_b_coef(const double* stats, const dou
   if (use_gn) {
     const double n = (double)C * (double)HW;
     double t1, t2, su, sux;
-    wave_seq_sum2(stats + (size_t)b * tps * 2, tps, &t1, &t2);
-    wave_seq_sum2(part + (size_t)b * nbands * (2 + 2 * C), nbands, &su, &sux, 2 + 2 * C);
+    wave_sum2(stats + (size_t)b * tps * 2, tps, &t1, &t2);
+    wave_sum2(part + (size_t)b * nbands * (2 + 2 * C), nbands, &su, &sux, 2 + 2 * C);
     const double m = t1 / n;
     double var = t2 / n - m * m;
     if (var < 0.0) var = 0.0;

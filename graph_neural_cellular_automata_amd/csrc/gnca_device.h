@@ -117,33 +117,35 @@ __device__ __forceinline__ void seq_sum2(const double* p, int n, int stride, dou
   *s1 = b;
 }
 
-// seq_sum2's sums (same order, same bits) computed by one whole wave: lane t loads pairs t,
-// t+64, ... (up to 256 pairs in one memory latency), then the pairs are added in index order
-// through lane broadcasts.  Every lane of the wave must call it; all get the sums.
-__device__ __forceinline__ void wave_seq_sum2(const double* p, int n, double* s0, double* s1,
-                                              int stride = 2) {
-  constexpr int PJ = 4;
-  if (n > 64 * PJ) {
-    seq_sum2(p, n, stride, s0, s1);
-    return;
-  }
+// Deterministic sums of the pairs p[stride*t], p[stride*t + 1], t < n, by one whole wave: lane l
+// adds pairs l, l+64, l+128, ... in that order (4 loads in flight per lane), then a fixed xor
+// butterfly combines the lanes.  The order depends only on n, so every consumer of the same
+// partials (K2, the backward's BA / BS) gets the same bits.  Every lane of the wave must call
+// it; all get the sums.
+__device__ __forceinline__ void wave_sum2(const double* p, int n, double* s0, double* s1,
+                                          int stride = 2) {
   const int lane = threadIdx.x & 63;
-  double a[PJ], b[PJ];
-#pragma unroll
-  for (int j = 0; j < PJ; ++j) {
-    const int t = lane + 64 * j;
-    a[j] = t < n ? p[(size_t)stride * t] : 0.0;
-    b[j] = t < n ? p[(size_t)stride * t + 1] : 0.0;
-  }
   double x = 0.0, y = 0.0;
+  for (int t0 = lane; t0 < n; t0 += 4 * 64) {
+    double a[4], b[4];
 #pragma unroll
-  for (int j = 0; j < PJ; ++j)
-    for (int l = 0; l < 64 && 64 * j + l < n; ++l) {
-      x += __shfl(a[j], l);
-      y += __shfl(b[j], l);
+    for (int j = 0; j < 4; ++j) {
+      const int t = t0 + 64 * j;
+      a[j] = t < n ? p[(size_t)stride * t] : 0.0;
+      b[j] = t < n ? p[(size_t)stride * t + 1] : 0.0;
     }
-  *s0 = x;
-  *s1 = y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x += a[j];
+      y += b[j];
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    x += __shfl_xor(x, off);
+    y += __shfl_xor(y, off);
+  }
+  *s0 = __shfl(x, 0);   // lane 0's association order, on every lane
+  *s1 = __shfl(y, 0);
 }
 
 // Where the forward keeps its intermediates in the step workspace (gnca_step.hip:make_plan);

@@ -334,10 +334,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
     const int i0 = ty * TH, j0 = tx * TW;
     const float* xb = a.x + (size_t)b * C * HW;
     if (a.active && !a.active[b]) {   // inactive sample (masked step): nothing to update
-      if (tid == 0 && !msg_only) {
-        a.stats[(size_t)tile * 2 + 0] = 0.0;
-        a.stats[(size_t)tile * 2 + 1] = 0.0;
-      }
+      if (tid < 2 * NW && !msg_only) a.stats[(size_t)tile * 2 * NW + tid] = 0.0;
       continue;
     }
     __syncthreads();  // previous tile's LDS readers are done (and the fragment staging area)
@@ -746,36 +743,32 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
     }
 
     PROF_MARK(4);   // group loop
-    // ---- per-tile partials: fp64 wave shuffle, then across the waves in LDS ----
+    // ---- per-(tile, wave) GroupNorm partials: fp64 wave shuffle, no workgroup barrier (K2 and
+    //      the backward add the NW pairs of every tile in a fixed order) ----
     if (GNCA_ABLATE & kAblReduce) continue;
-    double d1 = s1, d2 = s2;
     if (!msg_only) {
+      double d1 = s1, d2 = s2;
       for (int off = 32; off > 0; off >>= 1) {
         d1 += __shfl_xor(d1, off);
         d2 += __shfl_xor(d2, off);
       }
+      if (lane == 0) {
+        a.stats[((size_t)tile * NW + wave) * 2 + 0] = d1;
+        a.stats[((size_t)tile * NW + wave) * 2 + 1] = d2;
+      }
     }
-    if (want_attn) {
+    if (want_attn) {   // attention min / max per tile (runtime-geometry variants only)
       for (int off = 32; off > 0; off >>= 1) {
         amin = fminf(amin, __shfl_xor(amin, off));
         amax = fmaxf(amax, __shfl_xor(amax, off));
       }
-    }
-    double* redd = reinterpret_cast<double*>(red);
-    if (lane == 0) {
-      redd[wave * 2 + 0] = d1;
-      redd[wave * 2 + 1] = d2;
-      red[4 * NW + wave * 2 + 0] = amin;
-      red[4 * NW + wave * 2 + 1] = amax;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      if (!msg_only) {
-        double t1 = 0.0, t2 = 0.0;
-        for (int w = 0; w < NW; ++w) { t1 += redd[w * 2]; t2 += redd[w * 2 + 1]; }
-        a.stats[(size_t)tile * 2 + 0] = t1;
-        a.stats[(size_t)tile * 2 + 1] = t2;
+      if (lane == 0) {
+        red[4 * NW + wave * 2 + 0] = amin;
+        red[4 * NW + wave * 2 + 1] = amax;
       }
+      __syncthreads();
+    }
+    if (tid == 0) {
       if (want_attn) {
         float mn = INFINITY, mx = -INFINITY;
         for (int w = 0; w < NW; ++w) {
@@ -939,10 +932,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_2ph(const K1Args a) {
     const int i0 = ty * TH, j0 = tx * TW;
     const float* xb = a.x + (size_t)b * C * HW;
     if (a.active && !a.active[b]) {
-      if (tid == 0) {
-        a.stats[(size_t)tile * 2 + 0] = 0.0;
-        a.stats[(size_t)tile * 2 + 1] = 0.0;
-      }
+      if (tid < 2 * NW) a.stats[(size_t)tile * 2 * NW + tid] = 0.0;
       continue;
     }
     const size_t cell0 = (size_t)i0 * W + j0;
@@ -1200,7 +1190,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_2ph(const K1Args a) {
         ps2[gi] = s2;
       }
     }
-    // ---- per-tile partials: fp64 wave shuffle, then across the waves in LDS ----
+    // ---- per-(tile, wave) GroupNorm partials ----
     float t1 = 0.f, t2 = 0.f;
 #pragma unroll
     for (int gi = 0; gi < GPW; ++gi)
@@ -1213,17 +1203,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_2ph(const K1Args a) {
       d1 += __shfl_xor(d1, off);
       d2 += __shfl_xor(d2, off);
     }
-    double* redd = reinterpret_cast<double*>(red);
-    if (lane == 0) {
-      redd[wave * 2 + 0] = d1;
-      redd[wave * 2 + 1] = d2;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      double u1 = 0.0, u2 = 0.0;
-      for (int w_ = 0; w_ < NW; ++w_) { u1 += redd[w_ * 2]; u2 += redd[w_ * 2 + 1]; }
-      a.stats[(size_t)tile * 2 + 0] = u1;
-      a.stats[(size_t)tile * 2 + 1] = u2;
+    if (lane == 0) {   // per-(tile, wave) partials, as gnca_k1_update
+      a.stats[((size_t)tile * NW + wave) * 2 + 0] = d1;
+      a.stats[((size_t)tile * NW + wave) * 2 + 1] = d2;
     }
   }
 }
@@ -1241,6 +1223,7 @@ struct K2Args {
   float* attn;           // normalise in place if non-null
   const float* attn_mm;  // [B * tps * 2]
   int B, C, H, W, tps, band, nbands;
+  int nst;                 // GroupNorm partial pairs per sample (tps x waves per K1 workgroup)
   float gain, thr, eps;
   int use_gn;
   const uint8_t* active;   // [B] or null: inactive samples are copied through unchanged
@@ -1274,13 +1257,8 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   float* post = smem + (size_t)(a.band + 2) * W;     // [(r1-r0) x W] post-update alive mask
   float* gsh = sh_norm + 4;                          // gamma[C], then beta[C] at +32
 
-  // (1) loads: partials (wave 0), gamma/beta, alpha rows, the first main items
-  double p1 = 0.0, p2 = 0.0;
-  if (wave == 0 && gn)
-    for (int t = lane; t < a.tps && t < 64; t += 64) {
-      p1 = a.stats[((size_t)b * a.tps + t) * 2 + 0];
-      p2 = a.stats[((size_t)b * a.tps + t) * 2 + 1];
-    }
+  // (1) loads: gamma/beta, alpha rows, the first main items (the partials follow below; all in
+  //     flight together)
   float gam = 1.f, bet = 0.f;
   if (gn && tid < C) { gam = a.gamma[tid]; bet = a.beta[tid]; }
   const int na = (h1 - h0) * W;
@@ -1312,19 +1290,12 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   };
   load_items(tid);
 
-  // (2) per-sample statistics (fixed order: seq_sum2's, bit-reproducible)
+  // (2) per-sample statistics (wave_sum2: fixed order, bit-reproducible)
   if (wave == 0) {
     float mu = 0.f, rs = 1.f;
     if (gn) {
-      double t1 = 0.0, t2 = 0.0;
-      if (a.tps <= 64) {
-        for (int t = 0; t < a.tps; ++t) {
-          t1 += __shfl(p1, t);
-          t2 += __shfl(p2, t);
-        }
-      } else {
-        seq_sum2(a.stats + (size_t)b * a.tps * 2, a.tps, 2, &t1, &t2);
-      }
+      double t1, t2;
+      wave_sum2(a.stats + (size_t)b * a.nst * 2, a.nst, &t1, &t2);
       const double n = (double)C * (double)HW;
       const double m = t1 / n;
       double var = t2 / n - m * m;
@@ -1630,6 +1601,7 @@ static const Variant* find_variant(int C, int Hd) {
 struct Plan {
   const Variant* var;
   int k, RY, RX, TH, TW, tiles_x, tiles_y, tps, total_tiles;
+  int ppt;   // GroupNorm partial pairs per tile: one per K1 wave
   size_t lds1;
   bool graph_on, need_k0;
   // K2
@@ -1744,6 +1716,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->tiles_y = (d->H + bth - 1) / bth;
   P->tps = P->tiles_x * P->tiles_y;
   P->total_tiles = P->tps * d->B;
+  P->ppt = P->var->NT / 64;
   // K2 bands: ~6 row bands per sample (many small workgroups: no wave-quantisation tail),
   // each with its alpha rows + 2 halo rows and its post mask in LDS (<= 48 KB)
   {
@@ -1771,7 +1744,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   auto carve = [&o](size_t bytes) { size_t at = o; o += (bytes + 255) & ~(size_t)255; return at; };
   const size_t n = (size_t)d->B * d->C * d->H * d->W;
   P->off_dx = carve(msg_only ? 0 : n * 4);
-  P->off_stats = carve((size_t)P->total_tiles * 2 * sizeof(double));
+  P->off_stats = carve((size_t)P->total_tiles * P->ppt * 2 * sizeof(double));
   P->off_mm = carve((size_t)P->total_tiles * 2 * sizeof(float));
   P->off_offw = carve((size_t)d->B * (P->k > 0 ? P->k : 1) * sizeof(float));
   P->ws_bytes = o;
@@ -1793,7 +1766,7 @@ bool fwd_layout(const gnca_step_desc* d, FwdLayout* out) {
   out->off_dx = P.off_dx;
   out->off_stats = P.off_stats;
   out->off_offw = P.off_offw;
-  out->tps = P.tps;
+  out->tps = P.tps * P.ppt;   // GroupNorm partial pairs per sample
   out->k = P.k;
   out->graph_on = P.graph_on;
   out->need_k0 = P.need_k0;
@@ -1957,7 +1930,7 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   k2.gamma = w->gn_weight; k2.beta = w->gn_bias;
   k2.attn = (want_attn && P.graph_on) ? attn : nullptr;
   k2.attn_mm = reinterpret_cast<const float*>(wsb + P.off_mm);
-  k2.B = d->B; k2.C = d->C; k2.H = d->H; k2.W = d->W; k2.tps = P.tps;
+  k2.B = d->B; k2.C = d->C; k2.H = d->H; k2.W = d->W; k2.tps = P.tps; k2.nst = P.tps * P.ppt;
   k2.band = P.band; k2.nbands = P.nbands;
   k2.gain = d->update_gain; k2.thr = d->alpha_thr; k2.eps = d->gn_eps;
   k2.active = active;
