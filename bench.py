@@ -174,31 +174,57 @@ def cpu_baseline(budget_s: float, wl, H: int):
                       f"single-threaded; host CPU: {cpu}"}
 
 
+# The trainer configs (reference configs/config.json "training"/"damage" blocks): the graph
+# trainer's canvas for the headline train bench; BASELINE config 5 (32 ch, 128^2, r=5, K=16) adds
+# the damage curriculum and the classic trainer's stability phase (the graph
+# trainer's own stability block is dead code, train_graph_augmented_nca.py:342-360).
+TRAIN_WORKLOADS = {
+    "headline": dict(C=16, H=None, R=4, K=8, fixture="graph_torus_latest_grown_b1_72",
+                     damage=False, stability=False),
+    "c5": dict(C=32, H=128, R=5, K=16, fixture="graph_torus_c32_r5_k16_b1_48",
+               damage=True, stability=True),
+}
+DAMAGE_CFG = {"start_epoch": 100, "prob": 0.3,
+              "kinds": {"square": 0.35, "circle": 0.25, "stripes": 0.10, "alpha_drop": 0.15,
+                        "saltpepper": 0.05, "gaussian": 0.10},
+              "size_min": 6, "size_max": 18, "stripe_width": 6, "alpha_thr": 0.2,
+              "alpha_dropout_p": 0.15, "salt_pepper_p": 0.02, "gaussian_softness": 0.35,
+              "hidden_noise_sigma": 0.0}
+
+
 def main_train(args, dev, world, rank):
     """One data-parallel iteration of the graph trainer (train_graph_augmented_nca.py:289-391), on
     the package's device-side pieces: sample a batch from the device-resident pool (this rank's
-    shard of the 1024-slot pool), per-sample rollout lengths (48-80 steps), masked steps
-    (``active = nca_steps > t``: no sub-batch gather/scatter, no per-step host sync), fire rate
-    ~ U(0.5, 0.9) and the message on every 3rd step, premultiplied-RGBA MSE, loss.backward()
-    through the HIP step, one flat RCCL gradient all-reduce, per-parameter grad normalisation,
-    Adam, pool replace.  Weak scaling: ``--train-batch`` samples per GPU."""
+    shard of the 1024-slot pool), [config c5: the damage curriculum, damage.py:99-138],
+    per-sample rollout lengths (48-80 steps, or 200-400 with probability 0.4, config.json), masked
+    steps (``active = nca_steps > t``: no sub-batch gather/scatter, no per-step host sync), fire
+    rate ~ U(0.5, 0.9) and the message on every 3rd step, premultiplied-RGBA MSE, [config c5: the
+    classic trainer's stability phase, train_intermediate_loss.py:257-267: 24 more steps for the
+    samples already within 0.01 of the target, + 0.5 * their MSE], loss.backward() through the
+    HIP step, one flat RCCL gradient all-reduce, per-parameter grad normalisation, Adam, pool
+    replace.  Weak scaling: ``--train-batch`` samples per GPU."""
     import torch.distributed as dist
+    import torch.nn.functional as F
     from graph_neural_cellular_automata_amd import NeuralCAGraph
+    from graph_neural_cellular_automata_amd.damage import apply_damage_policy_
     from graph_neural_cellular_automata_amd.dp import allreduce_gradients, normalize_gradients_
     from graph_neural_cellular_automata_amd.pool import SamplePool
     from graph_neural_cellular_automata_amd.loss import loss_premult_rgba
-    wl = WORKLOADS["headline"]
-    C, R, K = wl["C"], wl["R"], wl["K"]
+    twl = TRAIN_WORKLOADS.get(args.config)
+    if twl is None:
+        raise SystemExit(f"--mode train supports --config headline|c5, not {args.config}")
+    C, R, K = twl["C"], twl["R"], twl["K"]
     torch.manual_seed(7)
     random.seed(42)                       # identical offset draws / fire rates on every rank
     model = NeuralCAGraph(C, HD, update_gain=GAIN, alpha_thr=THR, message_gain=MSG_GAIN,
                           graph_d_model=D_MODEL, graph_attention_radius=R, graph_num_neighbors=K,
                           graph_zero_padded_shift=False).to(dev)
-    model.load_state_dict({k: v for k, v in load_weights(dev, wl).items()}, strict=False)
+    model.load_state_dict({k: v for k, v in load_weights(dev, twl).items()}, strict=False)
     opt = torch.optim.Adam(model.parameters(), lr=2e-4, weight_decay=1e-5)
     params = [p for p in model.parameters() if p.requires_grad]
-    B, H = args.train_batch, args.train_size
-    lo_steps, hi_steps = 48, 80
+    B, H = args.train_batch, twl["H"] or args.train_size
+    short, long_, long_prob = (48, 80), (200, 400), 0.4
+    stats = {"long_rollouts": 0, "damage_calls": 0, "stability_samples": 0}
 
     def seed_fn(batch_size=1):            # train_graph_augmented_nca.py:108-114
         g = torch.zeros(batch_size, C, H, H, device=dev)
@@ -214,7 +240,12 @@ def main_train(args, dev, world, rank):
 
     def iteration():
         idx, state = pool.sample(B)
-        nsteps = torch.randint(lo_steps, hi_steps + 1, (B,), device=dev, generator=gen)
+        if twl["damage"]:
+            apply_damage_policy_(state, DAMAGE_CFG, epoch=DAMAGE_CFG["start_epoch"])
+            stats["damage_calls"] += 1
+        lo, hi = long_ if random.random() < long_prob else short
+        stats["long_rollouts"] += int(lo == long_[0])
+        nsteps = torch.randint(lo, hi + 1, (B,), device=dev, generator=gen)
         T = int(nsteps.max().item())
         for t in range(T):
             fr = random.uniform(0.5, 0.9)
@@ -222,13 +253,24 @@ def main_train(args, dev, world, rank):
             state = model(state, fire_rate=fr, active=nsteps > t)
         model.message_gain = MSG_GAIN
         cells[0] += int(nsteps.sum().item()) * H * H
-        loss = loss_premult_rgba(state[:, :4], target[None]).mean()   # fused HIP loss (fwd+bwd)
+        per_sample = loss_premult_rgba(state[:, :4], target[None])   # fused HIP loss (fwd+bwd)
+        loss = per_sample.mean()
+        if twl["stability"]:
+            close = (per_sample < 0.01).detach()
+            if bool(close.any()):
+                st = state
+                for _ in range(24):
+                    st = model(st, fire_rate=random.uniform(0.5, 1.0), active=close)
+                loss = loss + 0.5 * F.mse_loss(st[close, :4], target[None].expand(B, -1, -1, -1)[close])
+                n = int(close.sum().item())
+                stats["stability_samples"] += n
+                cells[0] += 24 * n * H * H
         opt.zero_grad(set_to_none=True)
         loss.backward()
         allreduce_gradients(params)
         normalize_gradients_(params)
         opt.step()
-        pool.replace(idx, state)
+        pool.replace(idx, state.detach())
         return loss
 
     for _ in range(args.warmup):
@@ -238,6 +280,8 @@ def main_train(args, dev, world, rank):
         dist.barrier()
     torch.cuda.synchronize()
     cells[0] = 0
+    for k_ in stats:
+        stats[k_] = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = iteration()
@@ -253,20 +297,27 @@ def main_train(args, dev, world, rank):
         el = float(tt.item())
         dist.all_reduce(tot)
     if rank == 0:
+        extra = ", damage curriculum (config.json), stability phase (24 steps, loss < 0.01)" \
+            if twl["damage"] else ""
         line = {
             "metric": "BPTT training cell-updates/sec (forward+backward through the CA step), "
                       "graph trainer iteration",
             "value": float(tot.item()) / el, "unit": "cell-updates/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic target; trainer seed states; trained nca_latest.pt weights (golden fixture)",
-            "config": {"workload": f"graph trainer iteration: device pool (1024/GPU), per-sample "
-                                   f"rollouts {lo_steps}-{hi_steps} steps via the masked step, fire "
-                                   f"U(0.5,0.9), message every 3rd step, premult-RGBA MSE, RCCL flat "
-                                   f"grad all-reduce, grad/||grad||, Adam, pool replace",
-                       "channels": C, "hidden": HD, "height": H, "width": H, "batch_per_gpu": B,
-                       "global_batch": B * world, "parallelism": f"dp{world}"},
+            "data": "synthetic target; trainer seed states; "
+                    + ("trained nca_latest.pt weights (golden fixture)" if C == 16 else
+                       "seeded random-init weights (golden fixture)"),
+            "config": {"workload": f"graph trainer iteration ({args.config}): device pool (1024/GPU), "
+                                   f"per-sample rollouts 48-80 steps (200-400 w.p. 0.4) via the masked "
+                                   f"step, fire U(0.5,0.9), message every 3rd step, premult-RGBA MSE"
+                                   f"{extra}, RCCL flat grad all-reduce, grad/||grad||, Adam, pool "
+                                   f"replace",
+                       "channels": C, "hidden": HD, "height": H, "width": H, "radius": R,
+                       "neighbors": K, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"dp{world}"},
             "iterations_per_s": args.steps / el, "final_loss": float(loss.detach()),
+            "iteration_stats": stats,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
