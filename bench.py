@@ -398,21 +398,25 @@ def main():
     cells = B * H * H
     value = cells * args.steps * world / el
 
-    # --- K1 (dominant, MFMA-bound) average duration with HIP events on the launch stream ---
+    # --- K1 (dominant, MFMA-bound) average duration with HIP events on the launch stream, in
+    #     the rollout's mode (K1 reads the alive masks the previous K2 wrote: PHASE_ALIVE) ---
     reps = 20
     d = make_desc(wl, B, H, H, rr.sample(offsets_table, K) if graph else [], rank, 0)
+    L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), x.data_ptr(), out.data_ptr(),
+                                     None, None, ws.data_ptr(), ws.numel(), sptr,
+                                     L.PHASE_ALL | L.PHASE_ALIVE), "prime")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
     ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
     for r in range(reps):
         ev[2 * r].record(stream)
         L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), out.data_ptr(),
                                          scratch.data_ptr(), None, None, ws.data_ptr(), ws.numel(),
-                                         sptr, L.PHASE_K1), "k1")
+                                         sptr, L.PHASE_K1 | L.PHASE_ALIVE), "k1")
         ev[2 * r + 1].record(stream)
         ev2[2 * r].record(stream)
         L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), out.data_ptr(),
                                          scratch.data_ptr(), None, None, ws.data_ptr(), ws.numel(),
-                                         sptr, L.PHASE_K2), "k2")
+                                         sptr, L.PHASE_K2 | L.PHASE_ALIVE), "k2")
         ev2[2 * r + 1].record(stream)
     torch.cuda.synchronize()
     k1_ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(reps))[reps // 2]

@@ -75,6 +75,7 @@ EXPORTS = ("gnca_abi_version", "gnca_status_string", "gnca_last_hip_error",
 
 PHASE_K0, PHASE_K1, PHASE_K2 = 1, 2, 4
 PHASE_ALL = 7
+PHASE_ALIVE = 8   # rollout mode: K2 hands the next step's alive masks to K1 (include/gnca.h)
 
 _lib = None
 

@@ -144,6 +144,8 @@ struct K1Args {
   const float* offw;   // [B * k] per-sample offset weights, or null -> uniform_w
   const void* fire;
   const uint8_t* active;   // [B] or null: samples with active[b] == 0 are skipped (K2 copies them)
+  const uint8_t* alive;    // [B,H,W] or null: this step's pre-update masks, written by the previous
+                           // step's K2 (bit 0: max-pool > alpha_thr, bit 1: > graph_alpha_thr)
   uint64_t seed;
   int64_t rng_step;
   int64_t sample_base;
@@ -399,6 +401,27 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
         }
       }
       }
+      if (DMA4 && a.alive) {
+        // the previous K2's alive bytes over the region (the post-update mask of step
+        // t is the pre-update mask of step t+1): one dword = 4 columns (W % 4 == 0, quad-aligned
+        // region), RH x RW/4 dwords instead of the (RH+2) x (RW+2) alpha plane
+        const uint8_t* ab = a.alive + (size_t)b * HW;
+        constexpr int QW = cRW / 4, NQA = cRH * QW, NIQ = (NQA + 63) / 64;
+#pragma unroll 1
+        for (int ii_ = wave; ii_ < NIQ; ii_ += NW) {
+          const int e = 64 * ii_ + lane;
+          int off = 0;
+          if (e < NQA) {
+            const int vr = e / QW, vc = 4 * (e - (e / QW) * QW);
+            int ii = i0 - RY + vr, jj = j0 - RX + vc;
+            ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
+            jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
+            off = ii * W + jj;
+          }
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ab + off),
+                                           (__attribute__((address_space(3))) void*)(al + 64 * ii_), 4, 0, 0);
+        }
+      } else {
       // alpha plane with one more ring: element e of ((RH+2) x ALW) -> (i0-RY-1+vr, j0-RX-1+vc)
 #pragma unroll 1
       for (int ii_ = wave; ii_ < NIA; ii_ += NW) {
@@ -422,6 +445,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(al + 64 * ii_),
                                          4, 0, 0);
+      }
       }
     }
     PROF_MARK(0);   // DMA issue
@@ -451,6 +475,20 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
     // ---- alive masks (max_pool 3x3 > thr, image-bounded, ncagraph.py:85-92): the sender plane
     //      (alive_to_alive ? A_graph : 1, zero where the source is off-image) over the region, and
     //      keep = pre-update alive AND fire for the tile cells ----
+    if (DMA4 && a.alive) {
+      const uint8_t* alb = reinterpret_cast<const uint8_t*>(al);   // region bytes, row-major
+#pragma unroll 1
+      for (int pos = tid; pos < ((GNCA_ABLATE & kAblPlanes) ? 0 : RH * RW); pos += NT) {
+        const int vr = pos / RW, vc = pos - (pos / RW) * RW;
+        const int v = alb[pos];
+        sp[pos] = a2a ? (float)((v >> 1) & 1) : 1.f;
+        const int ti = vr - RY, tj = vc - RX;
+        if (ti >= 0 && ti < TH && tj >= 0 && tj < TW) {
+          const int n = ti * TW + tj;
+          fp[n] = (v & 1) ? fp[n] : 0.f;
+        }
+      }
+    } else
 #pragma unroll 1
     for (int pos = tid; pos < ((GNCA_ABLATE & kAblPlanes) ? 0 : RH * RW); pos += NT) {
       const int vr = pos / RW, vc = pos - (pos / RW) * RW;
@@ -1224,7 +1262,8 @@ struct K2Args {
   const float* attn_mm;  // [B * tps * 2]
   int B, C, H, W, tps, band, nbands;
   int nst;                 // GroupNorm partial pairs per sample (tps x waves per K1 workgroup)
-  float gain, thr, eps;
+  uint8_t* alive_out;      // [B,H,W] or null: next step's pre-update masks (bit 0: thr, bit 1: gthr)
+  float gain, thr, eps, gthr;
   int use_gn;
   const uint8_t* active;   // [B] or null: inactive samples are copied through unchanged
 };
@@ -1345,6 +1384,8 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
       if (j < W - 1) mx = fmaxf(mx, row[j + 1]);
     }
     post[e] = mx > a.thr ? 1.f : 0.f;
+    if (a.alive_out)   // valid as next step's masks for 0 <= thr <= gthr (host checks)
+      a.alive_out[(size_t)b * HW + (size_t)r0 * W + e] = (uint8_t)((mx > a.thr ? 1 : 0) | (mx > a.gthr ? 2 : 0));
   }
   __syncthreads();
 
@@ -1608,7 +1649,7 @@ struct Plan {
   int band, nbands, total2;
   size_t lds2;
   // workspace carve (bytes)
-  size_t off_dx, off_stats, off_mm, off_offw, ws_bytes;
+  size_t off_dx, off_stats, off_mm, off_offw, off_alive, ws_bytes;
 };
 
 static int max_lds_bytes() { return 160 * 1024; }
@@ -1747,6 +1788,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->off_stats = carve((size_t)P->total_tiles * P->ppt * 2 * sizeof(double));
   P->off_mm = carve((size_t)P->total_tiles * 2 * sizeof(float));
   P->off_offw = carve((size_t)d->B * (P->k > 0 ? P->k : 1) * sizeof(float));
+  P->off_alive = carve((size_t)d->B * d->H * d->W);   // rollout: K2 -> next K1 alive bytes
   P->ws_bytes = o;
   if (P->need_k0) {
     const size_t k0 = ((size_t)d->C * d->H + d->C + d->d_model + P->k) * sizeof(double);
@@ -1892,9 +1934,12 @@ static bool weights_ok(const gnca_step_desc* d, const gnca_weights* w, bool msg_
   return true;
 }
 
+// alive_in / alive_out (rollout only): the previous step's K2 hands this step's K1 its pre-update
+// masks as bytes, so K1 skips the alpha halo and the 3x3 max-pools.
 static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float* x, float* x_out,
                      const void* fire, float* attn, void* ws, size_t ws_bytes, hipStream_t st,
-                     uint32_t phases = GNCA_PHASE_ALL, const uint8_t* active = nullptr) {
+                     uint32_t phases = GNCA_PHASE_ALL, const uint8_t* active = nullptr,
+                     bool alive_in = false, bool alive_out = false) {
   Plan P;
   if (!make_plan(d, false, &P)) {
     if (d && d->C >= 4 && d->hidden > 0 && !find_variant(d->C, d->hidden)) return GNCA_ERR_UNSUPPORTED;
@@ -1920,6 +1965,8 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   float* dx = reinterpret_cast<float*>(wsb + P.off_dx);
   fill_k1(k1, d, w, P, x, dx, fire, want_attn ? attn : nullptr, wsb);
   k1.active = active;
+  uint8_t* alive = reinterpret_cast<uint8_t*>(wsb + P.off_alive);
+  k1.alive = alive_in ? alive : nullptr;
   if ((phases & GNCA_PHASE_K1) && (rc = launch_k1(k1, P, st)) != GNCA_OK) return rc;
   if (!(phases & GNCA_PHASE_K2)) return GNCA_OK;
   K2Args k2;
@@ -1933,6 +1980,8 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   k2.B = d->B; k2.C = d->C; k2.H = d->H; k2.W = d->W; k2.tps = P.tps; k2.nst = P.tps * P.ppt;
   k2.band = P.band; k2.nbands = P.nbands;
   k2.gain = d->update_gain; k2.thr = d->alpha_thr; k2.eps = d->gn_eps;
+  k2.gthr = d->graph_alpha_thr;
+  k2.alive_out = alive_out ? alive : nullptr;
   k2.active = active;
   hipLaunchKernelGGL(gnca_k2_finalize, dim3(P.total2), dim3(kThreads), P.lds2, st, k2);
   return check_launch();
@@ -1991,8 +2040,10 @@ int gnca_step_masked_f32(const gnca_step_desc* desc, const gnca_weights* w, cons
 int gnca_step_phases_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
                          float* x_out, const void* fire, float* attn, void* ws, size_t ws_bytes,
                          void* stream, uint32_t phases) {
+  const bool alive = (phases & GNCA_PHASE_ALIVE) && desc && desc->alpha_thr >= 0.f &&
+                     desc->graph_alpha_thr >= desc->alpha_thr;
   return step_impl(desc, w, x, x_out, fire, attn, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream),
-                   phases);
+                   phases, nullptr, alive, alive);
 }
 
 int gnca_message_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
@@ -2073,12 +2124,17 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
                           hipMemcpyDeviceToDevice, st) == hipSuccess ? GNCA_OK : GNCA_ERR_HIP;
   gnca_step_desc dt = *desc;
   dt.flags &= ~GNCA_ATTENTION;
+  // K2 -> next K1 alive masks: exact when 0 <= alpha_thr <= graph_alpha_thr (a cell with alpha
+  // above either threshold keeps its alpha through the post-update gate); and only
+  // when every step uses the same threshold pair (one desc for the whole rollout: yes)
+  const bool hand_alive = desc->alpha_thr >= 0.f && desc->graph_alpha_thr >= desc->alpha_thr;
   const float* src = x;
   for (int t = 0; t < steps; ++t) {
     float* dst = ((steps - 1 - t) % 2 == 0) ? x_final : scratch;
     dt.rng_step = desc->rng_step + t;
     if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(dt.offsets, offsets + (size_t)t * 2 * k, 2 * k);
-    const int rc = step_impl(&dt, w, src, dst, nullptr, nullptr, ws, ws_bytes, st);
+    const int rc = step_impl(&dt, w, src, dst, nullptr, nullptr, ws, ws_bytes, st, GNCA_PHASE_ALL,
+                             nullptr, hand_alive && t > 0, hand_alive && t + 1 < steps);
     if (rc != GNCA_OK) return rc;
     src = dst;
   }

@@ -144,6 +144,10 @@ int gnca_step_masked_f32(const gnca_step_desc* desc, const gnca_weights* w, cons
 #define GNCA_PHASE_K1 (1u << 1)  /* perceive + gather + MLP -> dx, partials */
 #define GNCA_PHASE_K2 (1u << 2)  /* GroupNorm + residual + alive gate       */
 #define GNCA_PHASE_ALL (GNCA_PHASE_K0 | GNCA_PHASE_K1 | GNCA_PHASE_K2)
+/* Rollout mode of the measurement hook: K2 writes the next step's alive masks into the workspace
+ * and K1 reads them (what gnca_rollout_f32 does for every step after the first; needs
+ * 0 <= alpha_thr <= graph_alpha_thr, and a K2 call with this bit on the same workspace first). */
+#define GNCA_PHASE_ALIVE (1u << 3)
 int gnca_step_phases_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
                          float* x_out, const void* fire, float* attn, void* ws, size_t ws_bytes,
                          void* stream, uint32_t phases);
