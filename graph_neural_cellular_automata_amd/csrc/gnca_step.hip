@@ -997,6 +997,25 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_2ph(const K1Args a) {
     };
     __syncthreads();   // previous tile's readers of xs / lst are done
     stage(0);
+    if (a.alive) {
+      // the previous K2's alive bytes over the region, one byte -> one dword per position
+      // (SURVEY a13), instead of the alpha plane with its extra ring
+      const uint8_t* ab = a.alive + (size_t)b * HW;
+#pragma unroll 1
+      for (int ii_ = wave; ii_ < NI; ii_ += NW) {
+        const int e = 64 * ii_ + lane;
+        int off = 0;
+        if (e < RH * RW) {
+          const int vr = e / RW, vc = e - (e / RW) * RW;
+          int ii = i0 - RY + vr, jj = j0 - RX + vc;
+          ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
+          jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
+          off = ii * W + jj;
+        }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ab + off),
+                                         (__attribute__((address_space(3))) void*)(al + 64 * ii_), 1, 0, 0);
+      }
+    } else
 #pragma unroll 1
     for (int ii_ = wave; ii_ < NIA; ii_ += NW) {
       const int e = 64 * ii_ + lane;
@@ -1027,6 +1046,20 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_2ph(const K1Args a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // sender plane over the region; keep = pre-alive AND fire over the tile
+    if (a.alive) {
+      const int* alw = reinterpret_cast<const int*>(al);
+#pragma unroll 1
+      for (int pos = tid; pos < RH * RW; pos += NT) {
+        const int vr = pos / RW, vc = pos - (pos / RW) * RW;
+        const int v = alw[pos] & 0xff;
+        sp[pos] = a2a ? (float)((v >> 1) & 1) : 1.f;
+        const int ti = vr - RY, tj = vc - RX;
+        if (ti >= 0 && ti < TH && tj >= 0 && tj < TW) {
+          const int n = ti * TW + tj;
+          fp[n] = (v & 1) ? fp[n] : 0.f;
+        }
+      }
+    } else
 #pragma unroll 1
     for (int pos = tid; pos < RH * RW; pos += NT) {
       const int vr = pos / RW, vc = pos - (pos / RW) * RW;

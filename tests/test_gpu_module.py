@@ -266,3 +266,13 @@ def test_c32_two_phase_path_vs_oracle(dev, msg):
     lo, _ = S.step(desc(32, 0), w, x[:32].contiguous())
     hi, _ = S.step(desc(32, 32), w, x[32:].contiguous())
     assert torch.equal(out, torch.cat([lo, hi]))
+    # the rollout (K2 hands each step's alive masks to the next K1) == repeated single steps
+    d0 = desc(B, 0)
+    d0.rng_step = 0
+    r = S.rollout(d0, w, x, 3, [offs] * 3)
+    cur = x
+    for t in range(3):
+        dt = desc(B, 0)
+        dt.rng_step = t
+        cur, _ = S.step(dt, w, cur)
+    assert torch.equal(r, cur)
