@@ -807,7 +807,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           dh[m][r] = hp[m][r] > 0.f ? dh[m][r] : 0.f;
-          hp[m][r] = hp[m][r] > 0.f ? hp[m][r] : (hp[m][r] != hp[m][r] ? hp[m][r] : 0.f);  // relu
+          hp[m][r] = __builtin_elementwise_maximum(hp[m][r], 0.f);   // relu (NaN stays NaN)
         }
       __builtin_amdgcn_sched_barrier(0);
       // -- dY = W1^T dh -> HBM (slot = f*CP + c -> plane f*C + c); FT independent chains --

@@ -155,9 +155,11 @@ struct K1Args {
   int odl[GNCA_MAX_OFFSETS];   // gather source delta in the staged region: dy*RW + dx (pad: dy*RW)
 };
 
-// ReLU with torch.relu's NaN semantics (NaN stays NaN).  Deliberately NOT inline asm: hipcc does
-// not insert the MFMA-result read hazard wait states around an asm statement.
-__device__ __forceinline__ float relu_nan(float v) { return v < 0.f ? 0.f : v; }
+// ReLU with torch.relu's NaN semantics (NaN stays NaN): IEEE maximum, one v_maximum3_f32 on gfx950
+// instead of a compare + select (the GEMM1 epilogue runs it on 32 accumulators per 16-cell group,
+// and every VALU instruction costs fp32 MFMA issue time on the shared datapath).  Not inline asm:
+// hipcc does not insert the MFMA-result read hazard wait states around an asm statement.
+__device__ __forceinline__ float relu_nan(float v) { return __builtin_elementwise_maximum(v, 0.f); }
 
 // tanh(x) = 1 - 2 / (exp(2x) + 1): v_exp + v_rcp; abs error ~2e-7 (saturates to +-1, NaN-preserving)
 __device__ __forceinline__ float fast_tanh(float x) {

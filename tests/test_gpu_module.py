@@ -58,6 +58,31 @@ def test_module_forward_rng_contract_and_values(dev, zp):
     assert not torch.equal(out, x)
 
 
+def test_relu_keeps_nan_like_torch(dev):
+    """A NaN hidden bias: torch.relu keeps NaN (ncagraph.py's update_net), so every updated cell's dx
+    is NaN and GroupNorm spreads it over the sample; a NaN-dropping max(h, 0) would not."""
+    m = _trained_like(dev)
+    with torch.no_grad():
+        m.update_net[0].bias[3] = float("nan")
+    x = _state(1, 16, 24, 24, dev)
+    st = torch.cuda.get_rng_state(dev)
+    fire = (torch.rand(1, 1, 24, 24, device=dev) <= 0.5).float()
+    torch.cuda.set_rng_state(st, dev)
+    random.seed(3)
+    chosen = random.sample(m.graph.offsets, 8)
+    random.seed(3)
+    with torch.no_grad():
+        out = m(x, fire_rate=0.5)
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    cfg = dict(update_gain=0.05, alpha_thr=0.12, use_groupnorm=True, graph=True,
+               message_gain=0.25, hidden_only=True, zero_padded_shift=False, alive_to_alive=True)
+    with np.errstate(invalid="ignore"):
+        ref = O.nca_step(x.cpu().numpy().astype(np.float64), p, cfg, chosen=chosen,
+                         fire_mask=fire.cpu().numpy().astype(np.float64))
+    assert np.isnan(ref).any()
+    np.testing.assert_array_equal(np.isnan(out.cpu().numpy()), np.isnan(ref))
+
+
 def test_torch_rng_consumed_only_when_fire_rate_below_one(dev):
     m = _trained_like(dev)
     x = _state(1, 16, 24, 24, dev)

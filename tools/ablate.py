@@ -71,6 +71,12 @@ def run(reps=15, rounds=3):
     d = bench.make_desc(wl, B, H, H, offs, 0)
     ws = torch.empty(next(iter(libs.values())).gnca_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream()
+    # rollout mode (default): K1 reads the alive bytes a primed K2 wrote (GNCA_PHASE_ALIVE)
+    ph = int(os.environ.get("ABLATE_PHASES", str(L.PHASE_K1 | L.PHASE_ALIVE)))
+    if ph & L.PHASE_ALIVE:
+        assert next(iter(libs.values())).gnca_step_phases_f32(
+            ctypes.byref(d), ctypes.byref(w), x.data_ptr(), out.data_ptr(), None, None, ws.data_ptr(),
+            ws.numel(), st.cuda_stream, L.PHASE_ALL | L.PHASE_ALIVE) == 0
     res = {n: [] for n in libs}
     for _ in range(rounds):
         for n, lib in libs.items():
@@ -78,7 +84,7 @@ def run(reps=15, rounds=3):
                 e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(st)
                 rc = lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), x.data_ptr(), out.data_ptr(),
-                                              None, None, ws.data_ptr(), ws.numel(), st.cuda_stream, 2)
+                                              None, None, ws.data_ptr(), ws.numel(), st.cuda_stream, ph)
                 e1.record(st)
                 assert rc == 0, (n, rc)
                 torch.cuda.synchronize()
@@ -94,7 +100,7 @@ def run(reps=15, rounds=3):
     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
     e0.record(st)
     assert pl.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), x.data_ptr(), out.data_ptr(), None,
-                                   None, ws.data_ptr(), ws.numel(), st.cuda_stream, 2) == 0
+                                   None, ws.data_ptr(), ws.numel(), st.cuda_stream, ph) == 0
     e1.record(st)
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * (1024 * 16))()
