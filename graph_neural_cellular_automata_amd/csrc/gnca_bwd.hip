@@ -524,7 +524,15 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       plo[ft][r] = (slot < 3 * CP && c < C) ? (f * C + c) * HWi : -1;
     }
   const bool cfull = C == CP;   // no padded channels: every output row is live
-  for (int tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+  // XCD-aware tile order (speed only), as K1: workgroups b and b+8 share an XCD under round-robin
+  // dispatch, so each XCD group sweeps a contiguous tile range and neighbouring tiles' halo
+  // re-reads hit that XCD's L2
+  const int nxcd = gridDim.x >= 8 ? 8 : 1;
+  const int xg_ = blockIdx.x % nxcd, xr_ = blockIdx.x / nxcd;
+  const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
+  const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
+  const int t_begin = xg_ * tq + min(xg_, trm), t_end = t_begin + tq + (xg_ < trm ? 1 : 0);
+  for (int tile = t_begin + xr_; tile < t_end; tile += per_x) {
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
@@ -1031,7 +1039,13 @@ __host__ __device__ inline int bc_stage(int TH, int TW, int RY, int RX, bool msg
 __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
-  const int cg = blockIdx.x % a.ncg, bt = blockIdx.x / a.ncg;
+  // XCD-aware order (speed only): workgroups are dispatched round-robin over the 8 XCDs, so
+  // workgroup w runs on XCD w % 8; give each XCD a contiguous range of (sample, tile, channel
+  // group) items, so neighbouring tiles' halo re-reads hit that XCD's L2 instead of HBM
+  const int G = (int)gridDim.x, xq = G / 8, xr = G % 8;
+  const int xcd = (int)blockIdx.x % 8, xj = (int)blockIdx.x / 8;
+  const int wid = G >= 8 ? xcd * xq + min(xcd, xr) + xj : (int)blockIdx.x;
+  const int cg = wid % a.ncg, bt = wid / a.ncg;
   const int b = bt / a.tps, tin = bt - b * a.tps;
   if (a.active && !a.active[b]) return;   // dY = dG = 0 for an inactive sample
   const int c_lo = cg * a.cpw, c_hi = min(a.C, c_lo + a.cpw);
@@ -1547,17 +1561,23 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   }
   // BC tiles: fewest padded cells + staged halo, within the per-thread staging registers
   {
-    static const int bth[] = {8, 12, 16, 24, 32};
-    static const int btw[] = {16, 24, 32, 48, 64};
+    static const int bth[] = {4, 6, 8, 12, 16, 24, 32};
+    const int btw[] = {16, 24, 32, 48, 64, W};   // W: full-width rows (contiguous line fills)
     const int rxc = P->zp ? 0 : rx;
     double bestc = 1e300;
     P->TH3 = 0;
+    // 128-byte lines touched by a staged row segment of n floats at an unaligned start
+    auto lines = [](int n) { return (n * 4 + 127) / 128 + 1; };
     for (int th : bth)
       for (int tw : btw) {
         const int se = bc_stage(th, tw, ry, rxc, P->msg);
         if (se > kBCStage * kThreads || th * tw > 4 * kThreads) continue;
         const long tx = (W + tw - 1) / tw, ty = (H + th - 1) / th;
-        const double cost = (double)tx * ty * (th * tw + 0.25 * se);
+        // per tile: its cells plus the cache lines its staging fills (3 dY planes with a 1-ring,
+        // the dG region with the gather halo), in floats
+        const double fill = 32.0 * (3.0 * (th + 2) * lines(tw + 2) +
+                                    (P->msg ? (double)(th + 2 * ry) * lines(tw + 2 * rxc) : 0.0));
+        const double cost = (double)tx * ty * (th * tw + 0.25 * fill);
         if (cost < bestc) { bestc = cost; P->TH3 = th; P->TW3 = tw; }
       }
     if (!P->TH3) return false;
