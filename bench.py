@@ -45,14 +45,18 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 WORKLOADS = {
     "headline": dict(graph=True, C=16, H=72, B=1024, R=4, K=8,
                      fixture="graph_torus_latest_grown_b1_72",
-                     name="graph-augmented NCA rollout, torus, r=4, K=8, fire 0.5"),
+                     name="graph-augmented NCA rollout, torus, r=4, K=8, fire 0.5",
+                     k1="gnca_k1_update<16,128,24,36,4,4,8,512>"),
     "c2": dict(graph=False, C=16, H=72, B=8, R=0, K=0, fixture="classic_ep980_b2_32",
-               name="classic NCA rollout (BASELINE config 2), fire 0.5"),
+               name="classic NCA rollout (BASELINE config 2), fire 0.5",
+               k1="gnca_k1_update<16,128,8,24,1,1,0,512>"),
     "c3": dict(graph=True, C=16, H=72, B=8, R=4, K=8, fixture="graph_torus_latest_grown_b1_72",
-               name="graph-augmented NCA rollout (BASELINE config 3), torus, r=4, K=8, fire 0.5"),
+               name="graph-augmented NCA rollout (BASELINE config 3), torus, r=4, K=8, fire 0.5",
+               k1="gnca_k1_update<16,128,8,24,4,4,8,512>"),
     "c5": dict(graph=True, C=32, H=128, B=128, R=5, K=16, fixture="graph_torus_c32_r5_k16_b1_48",
                name="graph-augmented NCA rollout (BASELINE config 5), 32ch, torus, r=5, K=16, "
-                    "fire 0.5, pool 1024 sharded 128/GPU"),
+                    "fire 0.5, pool 1024 sharded 128/GPU",
+               k1="gnca_k1_2ph<32,128,16,16,5,5,16>"),
 }
 # per-launch HBM traffic of K1/K2 measured by rocprofv3 PMC counters in separate passes
 # (tools/pmc.sh + tools/pmc_traffic.py); counters cannot be read from inside this process
@@ -430,7 +434,7 @@ def main():
     k1_flops = cells * fpc
     k2_bytes = cells * C * 4 * 3                   # read x, dx; write x'
     headline = args.config == "headline"
-    roof = {"bound": "mfma", "kernel": f"gnca_k1_update<{C},{HD}>",
+    roof = {"bound": "mfma", "kernel": wl.get("k1", f"gnca_k1_update<{C},{HD}>"),
             "achieved": k1_flops / (k1_ms * 1e-3) / 1e12,
             "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
             "frac": k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA,
