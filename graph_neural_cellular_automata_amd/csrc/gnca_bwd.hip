@@ -1065,42 +1065,40 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   float* wts = as_ + TH * TW;                          // [k]
   float* pws = wts + (k > 0 ? k : 1);                  // [C*27] perception weights
   const float* xb = a.x + (size_t)b * C * HW;
-  // per-thread staging plan: element e = tid + 256*i of [3 dY planes | dG halo]; source offset
-  // within the channel plane (or -1 = zero), and the plane group (0..2 dY, 3 dG)
+  // per-thread staging plan: element e = tid + 256*i of [3 dY planes | dG halo]. Per slot:
+  // the source offset from the channel's plane base (dY plane f adds f*C*HW; -1 = zero fill),
+  // and bit i of gsel set when the slot reads dG. Both are hoisted out of the channel loop, so
+  // a load costs one select of two wave-uniform bases plus one 64-bit add.
+  const int CHW = C * (int)HW;
   int soff[kBCStage];
-  int sgrp[kBCStage];
+  uint32_t gsel = 0;
 #pragma unroll
   for (int i = 0; i < kBCStage; ++i) {
     const int e = tid + kThreads * i;
     soff[i] = -1;
-    sgrp[i] = -1;
     if (e >= SE) continue;
     if (e < 3 * PA) {
       const int f = e / PA, r = e - f * PA;
       const int ii = i0 - 1 + r / PW, jj = j0 - 1 + r % PW;
-      sgrp[i] = f;
-      if (ii >= 0 && ii < H && jj >= 0 && jj < W) soff[i] = ii * W + jj;
+      if (ii >= 0 && ii < H && jj >= 0 && jj < W) soff[i] = f * CHW + ii * W + jj;
     } else {
       const int r = e - 3 * PA;
       int ii = i0 - RY + r / GW, jj = j0 - RX + r % GW;
       bool ok = true;
       if (zp) ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
       else { ii = wrapi(ii, H); jj = wrapi(jj, W); }
-      sgrp[i] = 3;
+      gsel |= 1u << i;
       if (ok) soff[i] = ii * W + jj;
     }
   }
   float stg[kBCStage];
   auto load = [&](int c) {
+    const float* pY = a.dY + ((size_t)b * 3 * C + c) * HW;
+    const float* pG = a.dG + ((size_t)b * C + c) * HW;
 #pragma unroll
     for (int i = 0; i < kBCStage; ++i) {
-      float v = 0.f;
-      if (soff[i] >= 0) {
-        const float* base = sgrp[i] < 3 ? a.dY + ((size_t)b * 3 * C + sgrp[i] * C + c) * HW
-                                        : a.dG + ((size_t)b * C + c) * HW;
-        v = base[soff[i]];
-      }
-      stg[i] = v;
+      const float* p = ((gsel >> i) & 1u) ? pG : pY;
+      stg[i] = soff[i] >= 0 ? p[soff[i]] : 0.f;
     }
   };
   auto store = [&](float* dst) {
@@ -1109,15 +1107,22 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
       if (tid + kThreads * i < SE) dst[tid + kThreads * i] = stg[i];
   };
   // gx is read-modify-written; its next-channel values are prefetched with the staging loads
-  // (th*tw <= 4*kThreads: at most 4 cells per thread)
+  // (th*tw <= 4*kThreads: at most 4 cells per thread). Per cell: offset in the channel plane
+  // (-1 = none) and the tile-local index ti*TW + tj, hoisted out of the channel loop.
+  int goff[4], gtij[4];   // gtij = ti << 16 | tj
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int n = tid + kThreads * u;
+    const int ti = n / TW, tj = n - (n / TW) * TW;
+    const int i = i0 + ti, j = j0 + tj;
+    gtij[u] = (ti << 16) | tj;
+    goff[u] = (n < TH * TW && i < H && j < W) ? i * W + j : -1;
+  }
   float gxc[4], gxn[4];
   auto load_gx = [&](int c, float* dst) {
+    const float* pg = a.gx + ((size_t)b * C + c) * HW;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int n = tid + kThreads * u;
-      const int i = i0 + n / TW, j = j0 + n % TW;
-      dst[u] = (n < TH * TW && i < H && j < W) ? a.gx[((size_t)b * C + c) * HW + (size_t)i * W + j] : 0.f;
-    }
+    for (int u = 0; u < 4; ++u) dst[u] = goff[u] >= 0 ? pg[goff[u]] : 0.f;
   };
   // the first channel's staging loads go out before the perception weights / sender mask, so
   // the prologue waits out one memory latency, not three
@@ -1153,13 +1158,12 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
       load_gx(c + 1, gxn);
     }
     const float* pw = pws + c * 27;
+    float* pgx = a.gx + ((size_t)b * C + c) * HW;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
+      if (goff[u] < 0) continue;
       const int n = tid + kThreads * u;
-      if (n >= TH * TW) continue;
-      const int ti = n / TW, tj = n % TW;
-      const int i = i0 + ti, j = j0 + tj;
-      if (i >= H || j >= W) continue;
+      const int ti = gtij[u] >> 16, tj = gtij[u] & 0xffff;
       // y(p) += w[u][v] x(p + (u-1, v-1))  =>  gx(q) += w[u][v] dY(q - (u-1, v-1))
       float acc = 0.f;
 #pragma unroll
@@ -1179,7 +1183,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
         }
         acc = fmaf(as_[n], sg, acc);
       }
-      a.gx[((size_t)b * C + c) * HW + (size_t)i * W + j] = gxc[u] + acc;
+      pgx[goff[u]] = gxc[u] + acc;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) gxc[u] = gxn[u];
