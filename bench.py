@@ -237,9 +237,14 @@ def main_train(args, dev, world, rank):
         return g
 
     pool = SamplePool(1024 * world, seed_fn, device=dev, shard=(rank, world))
-    gen = torch.Generator(device=dev).manual_seed(99 + rank)
-    target = torch.rand(4, H, H, device=dev, generator=gen)
+    # one target for the whole job (every rank trains the same objective); per-rank rollout
+    # lengths come from a per-rank generator (each rank's samples are its own)
+    target = torch.rand(4, H, H, device=dev, generator=torch.Generator(device=dev).manual_seed(99))
     target[:3] *= target[3:4]
+    gen = torch.Generator(device=dev).manual_seed(100 + rank)
+    # the stability phase's fire rates: a private stream, so the shared global `random` stream
+    # (offset draws, fire rates, short/long regime) stays in lockstep on every rank
+    stab_rng = random.Random(4242 + rank)
     cells = [0]
 
     def iteration():
@@ -261,12 +266,18 @@ def main_train(args, dev, world, rank):
         loss = per_sample.mean()
         if twl["stability"]:
             close = (per_sample < 0.01).detach()
-            if bool(close.any()):
+            n = int(close.sum().item())
+            run = n > 0
+            if world > 1:   # one decision for the job: every rank runs the phase or none does
+                flag = torch.tensor([float(n)], device=dev if args.dist_backend == "nccl" else "cpu")
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                run = flag.item() > 0
+            if run:
                 st = state
                 for _ in range(24):
-                    st = model(st, fire_rate=random.uniform(0.5, 1.0), active=close)
-                loss = loss + 0.5 * F.mse_loss(st[close, :4], target[None].expand(B, -1, -1, -1)[close])
-                n = int(close.sum().item())
+                    st = model(st, fire_rate=stab_rng.uniform(0.5, 1.0), active=close)
+                if n > 0:
+                    loss = loss + 0.5 * F.mse_loss(st[close, :4], target[None].expand(B, -1, -1, -1)[close])
                 stats["stability_samples"] += n
                 cells[0] += 24 * n * H * H
         opt.zero_grad(set_to_none=True)

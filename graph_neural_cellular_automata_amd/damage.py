@@ -113,40 +113,48 @@ def gaussian_hole_(state, radius: int, softness: float = 0.35):
     _launch(state, L.DMG_GAUSSIAN, radius, pos=_centres(B, H, W, radius, state.device), softness=softness)
 
 
+def _cfg(cfg: dict, key: str, legacy: str | None, default):
+    """``cfg[key]``, else the older key name the reference also accepts, else ``default``."""
+    if key in cfg:
+        return cfg[key]
+    if legacy is not None and legacy in cfg:
+        return cfg[legacy]
+    return default
+
+
+# kind -> launcher(state, size, knobs).  ``size`` is the policy's sampled patch size; ``knobs``
+# the parsed config (damage.py:118-136 maps each kind to one of the primitives above).
+_KINDS = {
+    "square": lambda st, n, k: cutout_square_(st, n),
+    "circle": lambda st, n, k: cutout_circle_(st, n // 2 if n > 1 else 1),
+    "stripes": lambda st, n, k: stripe_wipe_(st, k["stripe_width"], orientation="auto"),
+    "alpha_drop": lambda st, n, k: alpha_dropout_(st, k["alpha_dropout_p"], alpha_thr=k["alpha_thr"], hard=True),
+    "saltpepper": lambda st, n, k: salt_pepper_alpha_(st, k["salt_pepper_p"]),
+    "gaussian": lambda st, n, k: gaussian_hole_(st, radius=max(1, n // 2), softness=k["gaussian_softness"]),
+    "hidden_noise": lambda st, n, k: hidden_scramble_(st, sigma=k["hidden_noise_sigma"]),
+}
+
+
 @torch.no_grad()
 def apply_damage_policy_(state, dmg_cfg: dict, epoch: int):
-    """The reference's policy (damage.py:99-138): one sampled kind for the whole batch."""
-    start_ep = int(dmg_cfg.get("start_epoch", dmg_cfg.get("damage_start_epoch", 100)))
-    prob = float(dmg_cfg.get("prob", dmg_cfg.get("damage_prob", 0.0)))
-    if epoch < start_ep or prob <= 0:
+    """The reference's policy (damage.py:99-138): from ``start_epoch`` on, with probability
+    ``prob`` (one device ``torch.rand(1)``), ONE kind for the whole batch drawn by
+    ``random.choices`` over ``kinds``, a patch size by ``random.randint(size_min, size_max)``, then
+    that kind's primitive; an unknown kind falls back to the square cut-out.  Same draws, in the
+    same order, as the reference."""
+    if epoch < int(_cfg(dmg_cfg, "start_epoch", "damage_start_epoch", 100)):
         return
-    if torch.rand(1, device=state.device).item() > prob:
+    prob = float(_cfg(dmg_cfg, "prob", "damage_prob", 0.0))
+    if prob <= 0 or torch.rand(1, device=state.device).item() > prob:
         return
-    kinds = dmg_cfg.get("kinds", {"square": 1.0})
-    names, weights = zip(*kinds.items())
-    kind = random.choices(names, weights=weights, k=1)[0]
-    size_min = int(dmg_cfg.get("size_min", dmg_cfg.get("damage_patch_size", 8)))
-    size_max = int(dmg_cfg.get("size_max", max(size_min, 14)))
-    size = int(random.randint(size_min, size_max))
-    alpha_thr = float(dmg_cfg.get("alpha_thr", 0.1))
-    alpha_drop_p = float(dmg_cfg.get("alpha_dropout_p", 0.1))
-    stripe_width = int(dmg_cfg.get("stripe_width", size))
-    saltpepper_p = float(dmg_cfg.get("salt_pepper_p", 0.02))
-    hidden_sigma = float(dmg_cfg.get("hidden_noise_sigma", 0.0))
-    gaussian_soft = float(dmg_cfg.get("gaussian_softness", 0.35))
-    if kind == "square":
-        cutout_square_(state, size)
-    elif kind == "circle":
-        cutout_circle_(state, size // 2 if size > 1 else 1)
-    elif kind == "stripes":
-        stripe_wipe_(state, stripe_width, orientation="auto")
-    elif kind == "alpha_drop":
-        alpha_dropout_(state, alpha_drop_p, alpha_thr=alpha_thr, hard=True)
-    elif kind == "saltpepper":
-        salt_pepper_alpha_(state, saltpepper_p)
-    elif kind == "gaussian":
-        gaussian_hole_(state, radius=max(1, size // 2), softness=gaussian_soft)
-    elif kind == "hidden_noise":
-        hidden_scramble_(state, sigma=hidden_sigma)
-    else:
-        cutout_square_(state, size)
+    table = dmg_cfg.get("kinds", {"square": 1.0})
+    kind = random.choices(list(table.keys()), weights=list(table.values()), k=1)[0]
+    lo = int(_cfg(dmg_cfg, "size_min", "damage_patch_size", 8))
+    size = int(random.randint(lo, int(_cfg(dmg_cfg, "size_max", None, max(lo, 14)))))
+    knobs = {"alpha_thr": float(dmg_cfg.get("alpha_thr", 0.1)),
+             "alpha_dropout_p": float(dmg_cfg.get("alpha_dropout_p", 0.1)),
+             "stripe_width": int(dmg_cfg.get("stripe_width", size)),
+             "salt_pepper_p": float(dmg_cfg.get("salt_pepper_p", 0.02)),
+             "hidden_noise_sigma": float(dmg_cfg.get("hidden_noise_sigma", 0.0)),
+             "gaussian_softness": float(dmg_cfg.get("gaussian_softness", 0.35))}
+    _KINDS.get(kind, _KINDS["square"])(state, size, knobs)

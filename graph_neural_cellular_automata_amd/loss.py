@@ -47,17 +47,23 @@ class _PremultLoss(torch.autograd.Function):
 
 def loss_premult_rgba(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     """Per-sample [B] MSE between (pred_rgb * pred_alpha, pred_alpha) and target ([B or 1,4,H,W])."""
-    if pred.device.type != "cuda" or pred.dtype != torch.float32:
-        raise RuntimeError("loss_premult_rgba runs on a float32 ROCm tensor (no CPU path)")
     if pred.dim() != 4 or pred.shape[1] != 4:
         raise ValueError("pred must be [B,4,H,W]")
+    B, _, H, W = pred.shape
+    if target.dim() == 3:
+        target = target.unsqueeze(0)
+    # the kernels index the target with pred's geometry: reject what F.mse_loss could not
+    # broadcast (the reference raises there) instead of reading out of bounds on the device
+    if target.dim() != 4 or tuple(target.shape[1:]) != (4, H, W) or target.shape[0] not in (1, B):
+        raise ValueError(f"target of shape {tuple(target.shape)} does not match pred [{B},4,{H},{W}] "
+                         f"(expected [4,{H},{W}], [1,4,{H},{W}] or [{B},4,{H},{W}])")
+    if pred.device.type != "cuda" or pred.dtype != torch.float32:
+        raise RuntimeError("loss_premult_rgba runs on a float32 ROCm tensor (no CPU path)")
     if not _strided_ok(pred):
         pred = pred.contiguous()
     target = target.to(pred.device, torch.float32)
-    if target.dim() == 3:
-        target = target.unsqueeze(0)
     if target.shape[0] != 1 and target.stride(0) != 0:
         target = target.contiguous()
-    elif target.shape[0] == 1 or target.stride(0) == 0:
+    else:
         target = target[:1].contiguous()
     return _PremultLoss.apply(pred, target)

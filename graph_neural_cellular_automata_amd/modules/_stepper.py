@@ -63,14 +63,15 @@ def param_packs(model: nn.Module, tensors: dict | None = None):
     else:
         named = [(_SHORT_TO_NAME[k], t) for k, t in tensors.items() if k in _SHORT_TO_NAME]
     named = [(n, p) for n, p in named if p.requires_grad]
+    dev = named[0][1].device if named else None
     hit = _PACKS.get(model)
     if hit is not None and len(hit[0]) == len(named) and all(a is b for a, (_, b) in zip(hit[0], named)) \
-            and hit[2] == named[0][1].device:
+            and hit[2] == dev:
         return hit[1]
     core = [(n, p) for n, p in named if not n.startswith("graph.")]
     graph = [(n, p) for n, p in named if n.startswith("graph.")]
     packs = (_Pack(core) if core else None, _Pack(graph) if graph else None)
-    _PACKS[model] = (tuple(p for _, p in named), packs, named[0][1].device if named else None)
+    _PACKS[model] = (tuple(p for _, p in named), packs, dev)
     return packs
 
 
@@ -89,7 +90,8 @@ class _StepFn(torch.autograd.Function):
     backward's reduce kernel."""
 
     @staticmethod
-    def forward(ctx, x, desc, weights, keep, fire, want_attn, active, core, graph, tok_core, tok_graph):
+    def forward(ctx, x, desc, weights, keep, fire, want_attn, active, core, graph, tok_core, tok_graph,
+                tensors=None):
         ws = S.workspace(desc, x.device)   # kept: the backward reuses its update field
         out, attn = S.step(desc, weights, x, fire=fire, want_attention=want_attn, ws=ws, active=active)
         if attn is not None:
@@ -99,11 +101,21 @@ class _StepFn(torch.autograd.Function):
         ctx.ws = ws
         ctx.active = active
         ctx.packs = (core, graph)
+        # the weights are passed to the kernels as raw pointers (not saved tensors), so autograd's
+        # version check would not see an in-place update between forward and backward (an
+        # optimizer step, load_state_dict, EMA swap): record the versions and check them ourselves
+        ctx.versions = tuple((t, t._version) for t in (tensors or {}).values())
         return out, attn
 
     @staticmethod
     def backward(ctx, gout, gattn):
         (x,) = ctx.saved_tensors
+        for t, v in ctx.versions:
+            if t._version != v:
+                raise RuntimeError(
+                    "one of the variables needed for gradient computation has been modified by an "
+                    f"inplace operation: a step weight of shape {tuple(t.shape)} is at version "
+                    f"{t._version}; expected version {v} instead")
         desc = ctx.desc
         no_graph_use = (desc.flags & L.GRAPH) and desc.num_offsets == 0
         want, views, flats = {}, {}, [None, None]
@@ -117,7 +129,7 @@ class _StepFn(torch.autograd.Function):
                                 saved=ctx.ws, active=ctx.active, out=views)
         ctx.ws = None
         return (gx if ctx.needs_input_grad[0] else None, None, None, None, None, None, None, None, None,
-                flats[0], flats[1])
+                flats[0], flats[1], None)
 
 
 def apply_step(model: nn.Module, x, desc, weights, keep, fire, want_attn=False, active=None, tensors=None):
@@ -125,7 +137,7 @@ def apply_step(model: nn.Module, x, desc, weights, keep, fire, want_attn=False, 
     core, graph = param_packs(model, tensors)
     tc = core.token if core is not None else None
     tg = graph.token if graph is not None else None
-    return _StepFn.apply(x, desc, weights, keep, fire, want_attn, active, core, graph, tc, tg)
+    return _StepFn.apply(x, desc, weights, keep, fire, want_attn, active, core, graph, tc, tg, tensors)
 
 
 def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen, message_gain,

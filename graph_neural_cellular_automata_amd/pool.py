@@ -9,7 +9,11 @@ whole C4 pool (1024 x 16 x 72 x 72 fp32 = 340 MB) stays resident.
 
 Multi-GPU (``shard=(rank, world)``): each rank keeps only its contiguous slice of the pool
 (``sharding.shard_range``) and samples its share of the batch from it.  Every rank still calls
-``seed_fn`` for all P samples, so the global RNG streams stay identical across ranks.
+``seed_fn`` for all P samples, so the global RNG streams stay identical across ranks.  A sharded
+pool draws its slot indices from its own ``random.Random`` (seeded per rank), not from the global
+stream: slices may differ in length by one, and ``random.sample`` over different lengths consumes
+the stream differently, which would desynchronise the per-step offset draws that every rank must
+share (``sharding.py``).
 """
 from __future__ import annotations
 
@@ -33,6 +37,8 @@ class SamplePool:
             if i >= self.lo and i < self.hi:
                 seeds.append(s.reshape(s.shape[-3:]).to(device))
         self.states = torch.stack(seeds).contiguous() if seeds else torch.empty(0, device=device)
+        # unsharded: the global stream, exactly as the reference; sharded: a private stream
+        self._rng = random if world == 1 else random.Random(0x9E3779B9 * (rank + 1) + world)
 
     def __len__(self):
         return self.states.shape[0]
@@ -45,7 +51,7 @@ class SamplePool:
     def sample(self, batch_size):
         """(idx, batch): ``random.sample`` over this pool's slots (pool.py:23-32) and a fresh
         [B,C,H,W] tensor (a copy: the pool is not modified through it)."""
-        idx = random.sample(range(len(self)), batch_size)
+        idx = self._rng.sample(range(len(self)), batch_size)
         sel = torch.as_tensor(idx, dtype=torch.long, device=self.states.device)
         return idx, self.states.index_select(0, sel)
 

@@ -59,3 +59,30 @@ def test_unused_graph_pack_keeps_none_and_token_is_cached():
     assert core2 is core and graph2 is graph
     assert torch.equal(params["norm.bias"].grad, torch.full_like(params["norm.bias"], 1.0))
     assert torch.equal(params["graph.scaling"].grad, torch.full_like(params["graph.scaling"], 1.0))
+
+
+def test_frozen_model_has_no_packs_twice():
+    """All parameters frozen (input-gradient / saliency BPTT): no packs, and the cached empty
+    entry must not break the second step (IndexError on the cache check)."""
+    m = NeuralCAGraph(8, update_hidden=16)
+    m.requires_grad_(False)
+    assert param_packs(m) == (None, None)
+    assert param_packs(m) == (None, None)
+    m.requires_grad_(True)
+    core, graph = param_packs(m)
+    assert core is not None and graph is not None
+
+
+def test_loss_rejects_mismatched_target():
+    """The fused loss validates the target against pred before any device work (the reference's
+    F.mse_loss raises on a shape it cannot broadcast)."""
+    import pytest
+    from graph_neural_cellular_automata_amd.loss import loss_premult_rgba
+    pred = torch.zeros(3, 4, 8, 8)
+    for bad in (torch.zeros(3, 3, 8, 8), torch.zeros(3, 4, 8, 9), torch.zeros(2, 4, 8, 8),
+                torch.zeros(4, 7, 8), torch.zeros(8, 8)):
+        with pytest.raises(ValueError, match="does not match pred"):
+            loss_premult_rgba(pred, bad)
+    for ok in (torch.zeros(4, 8, 8), torch.zeros(1, 4, 8, 8), torch.zeros(3, 4, 8, 8)):
+        with pytest.raises(RuntimeError, match="no CPU path"):   # shape accepted, then no CPU path
+            loss_premult_rgba(pred, ok)

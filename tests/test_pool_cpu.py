@@ -61,3 +61,17 @@ def test_sharded_pool_slices_and_rng_stream():
         parts.append(p)
     assert [len(p) for p in parts] == [4, 3, 3]
     assert torch.equal(torch.cat([p.states for p in parts]), full.states)
+
+
+def test_sharded_pool_sampling_keeps_global_stream():
+    """Ranks whose slices differ in length must not desynchronise the global random stream (the
+    per-step offset draws are shared by every rank)."""
+    parts = [SamplePool(10, _seed_fn, shard=(r, 3)) for r in range(3)]
+    after = []
+    for p in parts:
+        random.seed(5)
+        idx, batch = p.sample(3)
+        assert len(set(idx)) == 3 and all(0 <= i < len(p) for i in idx)
+        assert batch.shape[0] == 3
+        after.append(random.random())
+    assert after[0] == after[1] == after[2]
