@@ -1,0 +1,560 @@
+// gnca_k1_split.h — K1 of the 16-channel / hidden-128 step on bf16 MFMA with an exact 3-way
+// split of every fp32 operand (included by gnca_step.hip after K1Args).
+//
+// Why.  gfx950 runs fp32 MFMA (v_mfma_f32_*_f32) at the fp32 VECTOR rate, 1/16 of bf16 MFMA,
+// and on the same SIMD datapath as VALU (profiles/r01_ubench_mfma_valu_overlap.txt).  The f32
+// K1 (gnca_k1_update) spends ~70 % of its group loop in fp32 MFMA issue.
+//
+// Numerics (fp32-class, not bf16).  Every fp32 operand v is split into three bf16 values
+// v = v0 + v1 + v2 EXACTLY (v0 = rne_bf16(v), v1 = rne_bf16(v - v0), v2 = v - v0 - v1: 8 + 8 + 8
+// significand bits hold the 24 of an fp32; for |v| > 2^-100 nothing is subnormal).  A dot
+// product a.b is then sum over (i, j) of a_i . b_j, and the kernel keeps the six terms with
+// i + j <= 2 (a0b0, a0b1, a1b0, a0b2, a2b0, a1b1): the dropped terms a1b2, a2b1, a2b2 are each
+// <= 2^-24 |a||b|, the size of one fp32 rounding.  bf16 x bf16 products are exact in fp32 and
+// the MFMA accumulates in fp32.  So each GEMM is an fp32 GEMM up to a few fp32 roundings per
+// product (measured against the f64 oracle in tests/test_gpu_*.py at the same tolerances as
+// the f32 kernel).  Cost: 6 bf16 products at 1/16 the cycles of one fp32 product = 0.375 of
+// the fp32 MFMA time, plus the VALU that splits the activations.
+//
+// MFMA: v_mfma_f32_32x32x16_bf16 (32 cycles, holds VALU issue for 8 of them).  Lane l: cell
+// l & 31 of a 32-cell group, channel / k half h = l >> 5.  Fragment maps
+// (cdna_hip_programming.md §3): A[row l&31][k 8h+j], B[k 8h+j][col l&31], D reg r ->
+// row (r&3) + 8(r>>2) + 4h, col l&31.
+//   GEMM1  H[128 x 32] = W1[128 x 48] Y[48 x 32] + b1: 4 row blocks (rb) x 3 k-chunks (kc);
+//          k slot (kc, h, j) = feature kc (0 id, 1 sobel-x, 2 sobel-y) of channel 8h + j, which
+//          is exactly W1's column 16 kc + 8h + j, so lane (cell, h) computes the perception of
+//          channels 8h..8h+7 of its own cell.  Bias: one extra MFMA per rb with A = the three
+//          bias parts in k slots 0..2 of lane half 0 and B = (1, 1, 1, 0, ...) on half 0, zeros
+//          on half 1 (so b1 enters exactly, and the accumulator starts at 0).
+//   GEMM2  DL[16 x 32] = W2[16 x 128] relu(H): k-chunk s = (rb, ss) takes accumulator registers
+//          8ss..8ss+7 of H block rb as the B fragment, element j of half h = hidden row
+//          32rb + 16ss + 8(j>>2) + 4h + (j&3) (no data movement; the A image is permuted to
+//          match).  M = 32 rows hold TWO 16-channel weight planes: A = [P0; P1] gives
+//          P0.H in rows 0-15 and P1.H in rows 16-31 of the SAME accumulator (one lane holds
+//          both: regs r and r + 8).  Products by B plane: H0 with P0, P1, P2; H1 with P0, P1;
+//          H2 with P0 -> accA += [P0;P1].H0 + [P0;P1].H1, accB += [P2;P2].H0 + [P0;P1].H2 (accB's
+//          rows 16-31 are ignored), dl = accA[r] + accA[r+8] + accB[r].
+//   MSG    M[16 x 32] = WM[16 x 16] G[16 x 32] (G = the gathered alive-masked x, k = channel
+//          8h + j): one k-chunk, stacks [M0;M1], [M2;0], [M0;0] (0 = a zero image), all in
+//          one accumulator: rows 0-15 + rows 16-31 = the six products.
+// Weight images (bf16, built once per persistent workgroup): W1 36 KB, bias 2 KB, W2 12 KB, WM
+// 1.5 KB + 0.5 KB of zeros; every A read is one conflict-free ds_read_b128.
+//
+// The rest of the tile pipeline is the f32 K1's (LDS-DMA staging, alive / sender / keep planes,
+// live-cell compaction, fp64 GroupNorm partials per (tile, wave)), with 32-cell groups, byte
+// keep plane, u16 live list and a tight channel-plane stride (DMA lanes past the region are
+// masked off instead of filling a pad).  Perception zero padding at the image border uses
+// per-tap LDS bases that point at a zero float (each plane's first pad float) instead of
+// per-channel selects.
+
+#pragma once
+
+namespace gnca {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// (a, b) -> three packed bf16x2 words with a = a0 + a1 + a2, b = b0 + b1 + b2 exactly (round to
+// nearest even at each level: NaN stays NaN in the leading part, v_cvt_pk_bf16_f32).
+__device__ __forceinline__ void split3_pair(float a, float b, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
+  const uint32_t h = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
+  const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+  const uint32_t m = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){ra, rb}, bf16x2v));
+  const float la = ra - __uint_as_float(m << 16), lb = rb - __uint_as_float(m & 0xffff0000u);
+  p0 = h;
+  p1 = m;
+  p2 = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){la, lb}, bf16x2v));
+}
+
+// 8 fp32 -> three bf16x8 fragments (k order = element order)
+__device__ __forceinline__ void split3_x8(const float* v, u32x4& f0, u32x4& f1, u32x4& f2) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t a, b, c;
+    split3_pair(v[2 * i], v[2 * i + 1], a, b, c);
+    f0[i] = a;
+    f1[i] = b;
+    f2[i] = c;
+  }
+}
+
+__device__ __forceinline__ f32x16 mfma_bx(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                 c, 0, 0, 0);
+}
+
+// channel-plane stride (floats) of the split kernel's staged region: at least one pad float
+// (the zero tap of the border perception), 16 mod 32 (planes start 16 banks apart), quads
+__host__ __device__ constexpr int ks_pstr(int rhw) {
+  int p = rhw + 1;
+  while (p % 32 != 16) ++p;
+  return p;
+}
+
+struct KSLayout {
+  int xs, sp, al, kp, lst, wcnt, red, w1, bias, w2, wm, wz, total;   // byte offsets
+};
+
+__host__ __device__ constexpr int ks_a16(int v) { return (v + 15) & ~15; }
+
+template <int TH, int TW, int RY, int RX>
+__host__ __device__ constexpr KSLayout ks_layout() {
+  constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
+  constexpr int ALW = RW + 2, NIA = ((RH + 2) * ALW + 63) / 64;
+  constexpr int NQA = RH * (RW / 4), NIQ = (NQA + 63) / 64;
+  KSLayout L{};
+  int o = 0;
+  L.xs = o; o += 16 * ks_pstr(RHW) * 4;   // first: region reads fit the 16-bit DS offsets
+  L.sp = o; o += ks_a16(RHW * 4);
+  L.al = o; o += 64 * 4 * (NIA > NIQ ? NIA : NIQ);
+  L.kp = o; o += ks_a16(TH * TW);
+  L.lst = o; o += ks_a16(TH * TW * 2);
+  L.wcnt = o; o += 32;
+  L.red = o; o += 256;
+  L.w1 = o; o += 3 * 4 * 3 * 1024;       // [plane][rb][kc][lane] x 16 B
+  L.bias = o; o += 4 * 32 * 16;          // [rb][row] x 16 B (k slots 0..2 = the three parts)
+  L.w2 = o; o += 3 * 8 * 2 * 16 * 16;    // [plane][s][h][channel] x 16 B
+  L.wm = o; o += 3 * 2 * 16 * 16;        // [plane][h][channel] x 16 B
+  L.wz = o; o += 2 * 16 * 16;            // zeros, laid out like one WM plane
+  L.total = o;
+  return L;
+}
+
+template <int TH, int TW, int RY, int RX, int KU>
+__global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_b[];
+  constexpr int C = 16, HD = 128, NT = 512, NW = 8;
+  constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
+  constexpr int PSTR = ks_pstr(RHW);
+  constexpr int NQ = RHW / 4, NI4 = (NQ + 63) / 64;
+  constexpr int ALW = RW + 2, NIA = ((RH + 2) * ALW + 63) / 64;
+  constexpr int QW = RW / 4, NQA = RH * QW, NIQ = (NQA + 63) / 64;
+  constexpr int NCELL = TH * TW;
+  constexpr KSLayout L = ks_layout<TH, TW, RY, RX>();
+  static_assert(RW % 4 == 0 && RX % 4 == 0 && TW % 4 == 0, "16-byte staging rows");
+  static_assert(RY >= 1 && RX >= 1, "perception halo");
+  static_assert(L.total <= 160 * 1024, "LDS");
+  static_assert(7 * PSTR * 4 + 4 * RHW < 65536, "channel offsets fit the DS immediate");
+  constexpr bool GRAPH = KU > 0;
+
+  float* xs = reinterpret_cast<float*>(smem_b + L.xs);
+  float* sp = reinterpret_cast<float*>(smem_b + L.sp);
+  float* al = reinterpret_cast<float*>(smem_b + L.al);
+  uint8_t* kp = reinterpret_cast<uint8_t*>(smem_b + L.kp);
+  uint16_t* lst = reinterpret_cast<uint16_t*>(smem_b + L.lst);
+  int* wcnt = reinterpret_cast<int*>(smem_b + L.wcnt);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r32 = lane & 31, c16 = lane & 15;
+  const int H = a.H, W = a.W;
+  const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
+  const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
+  const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
+
+  // ---- weight images (bf16 parts in MFMA fragment order), once per persistent workgroup ----
+  {
+    // W1: entry e = (rb, kc, lane): W1[32rb + (lane&31)][16kc + 8(lane>>5) + 0..7]
+    for (int e = tid; e < 4 * 3 * 64; e += NT) {
+      const int rb = e / 192, kc = (e / 64) % 3, l = e & 63;
+      const float* src = a.w1 + (size_t)(32 * rb + (l & 31)) * 48 + 16 * kc + 8 * (l >> 5);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = src[j];
+      u32x4 f0, f1, f2;
+      split3_x8(v, f0, f1, f2);
+      const int img = (rb * 3 + kc) * 1024 + l * 16;
+      *reinterpret_cast<u32x4*>(smem_b + L.w1 + 0 * 12288 + img) = f0;
+      *reinterpret_cast<u32x4*>(smem_b + L.w1 + 1 * 12288 + img) = f1;
+      *reinterpret_cast<u32x4*>(smem_b + L.w1 + 2 * 12288 + img) = f2;
+    }
+    // bias: entry (rb, row): k slots 0..2 = the parts of b1[32rb + row]
+    for (int e = tid; e < 128; e += NT) {
+      uint32_t p0, p1, p2;
+      split3_pair(a.b1[e], 0.f, p0, p1, p2);
+      u32x4 f;
+      f[0] = (p0 & 0xffffu) | (p1 << 16);
+      f[1] = p2 & 0xffffu;
+      f[2] = 0u;
+      f[3] = 0u;
+      *reinterpret_cast<u32x4*>(smem_b + L.bias + e * 16) = f;
+    }
+    // W2: entry (s, h, c): W2[c][32(s>>1) + 16(s&1) + 8(j>>2) + 4h + (j&3)], j = 0..7
+    for (int e = tid; e < 8 * 2 * 16; e += NT) {
+      const int s = e >> 5, hh = (e >> 4) & 1, c = e & 15;
+      const float* src = a.w2 + (size_t)c * HD + 32 * (s >> 1) + 16 * (s & 1) + 4 * hh;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = src[8 * (j >> 2) + (j & 3)];
+      u32x4 f0, f1, f2;
+      split3_x8(v, f0, f1, f2);
+      *reinterpret_cast<u32x4*>(smem_b + L.w2 + 0 * 4096 + e * 16) = f0;
+      *reinterpret_cast<u32x4*>(smem_b + L.w2 + 1 * 4096 + e * 16) = f1;
+      *reinterpret_cast<u32x4*>(smem_b + L.w2 + 2 * 4096 + e * 16) = f2;
+    }
+    // WM: entry (h, c): WM[c][8h + 0..7]; then the zero image
+    for (int e = tid; e < 32; e += NT) {
+      const int hh = e >> 4, c = e & 15;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = GRAPH ? a.wm[c * C + 8 * hh + j] : 0.f;
+      u32x4 f0, f1, f2;
+      split3_x8(v, f0, f1, f2);
+      *reinterpret_cast<u32x4*>(smem_b + L.wm + 0 * 512 + e * 16) = f0;
+      *reinterpret_cast<u32x4*>(smem_b + L.wm + 1 * 512 + e * 16) = f1;
+      *reinterpret_cast<u32x4*>(smem_b + L.wm + 2 * 512 + e * 16) = f2;
+    }
+    for (int e = tid; e < 32; e += NT) *reinterpret_cast<u32x4*>(smem_b + L.wz + e * 16) = u32x4{0u, 0u, 0u, 0u};
+    // the perception zero tap: every channel plane's pad floats (never written by the staging)
+    for (int e = tid; e < 16 * (PSTR - RHW); e += NT) xs[(e / (PSTR - RHW)) * PSTR + RHW + e % (PSTR - RHW)] = 0.f;
+  }
+  // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch; the
+  // other case reads the weights from global memory, an uncommon slow path)
+  int ok = 1;
+  for (int idx = tid; idx < C * 27; idx += NT) {
+    const int e = idx % 27, f = e / 9, tap = e % 9, tr = tap / 3, tc = tap % 3;
+    float ref;
+    if (f == 0) ref = (tap == 4) ? 1.f : 0.f;
+    else if (f == 1) ref = (float)((tc == 0 ? 1 : (tc == 2 ? -1 : 0)) * (tr == 1 ? 2 : 1));
+    else ref = (float)((tr == 0 ? 1 : (tr == 2 ? -1 : 0)) * (tc == 1 ? 2 : 1));
+    if (a.perc[idx] != ref) ok = 0;
+  }
+  const bool sobel = __syncthreads_and(ok) != 0;   // also the barrier after the image stores
+
+  // per-lane constants: message fragments (stacks [M0;M1], [M2;0], [M0;0]), ones for the bias,
+  // message bias / gain of this lane's 8 output channels c = (r&3) + 8(r>>2) + 4h
+  u32x4 wmA = {0u, 0u, 0u, 0u}, wmB = wmA, wmC = wmA;
+  if (GRAPH) {
+    const int ent = (h * 16 + c16) * 16;
+    wmA = *reinterpret_cast<const u32x4*>(smem_b + L.wm + (r32 < 16 ? 0 : 512) + ent);
+    wmB = *reinterpret_cast<const u32x4*>(smem_b + (r32 < 16 ? L.wm + 1024 : L.wz) + ent);
+    wmC = *reinterpret_cast<const u32x4*>(smem_b + (r32 < 16 ? L.wm : L.wz) + ent);
+  }
+  const u32x4 ones = h == 0 ? u32x4{0x3f803f80u, 0x3f80u, 0u, 0u} : u32x4{0u, 0u, 0u, 0u};
+  float bmr[8], gainr[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int c = (r & 3) + 8 * (r >> 2) + 4 * h;
+    bmr[r] = GRAPH ? a.bm[c] : 0.f;
+    gainr[r] = (GRAPH && !(hidden_only && c < 4)) ? a.message_gain : 0.f;
+  }
+  // W2 A-fragment lane bases: T0 = [P0;P1], T1 = [P2;P2] (+ s * 512 per k-chunk)
+  const int w2T0 = L.w2 + (r32 < 16 ? 0 : 4096) + (h * 16 + c16) * 16;
+  const int w2T1 = L.w2 + 8192 + (h * 16 + c16) * 16;
+
+  const size_t HW = (size_t)H * W;
+
+  // XCD-aware tile order (as gnca_k1_update)
+  const int nxcd = gridDim.x >= 8 ? 8 : 1;
+  const int xg_ = blockIdx.x % nxcd, xr_ = blockIdx.x / nxcd;
+  const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
+  const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
+  const int t_begin = xg_ * tq + min(xg_, trm), t_end = t_begin + tq + (xg_ < trm ? 1 : 0);
+  for (int tile = t_begin + xr_; tile < t_end; tile += per_x) {
+    const int b = tile / a.tps, tin = tile - b * a.tps;
+    const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+    const int i0 = ty * TH, j0 = tx * TW;
+    const float* xb = a.x + (size_t)b * C * HW;
+    if (a.active && !a.active[b]) {   // inactive sample (masked step)
+      if (tid < 2 * NW) a.stats[(size_t)tile * 2 * NW + tid] = 0.0;
+      continue;
+    }
+    __syncthreads();   // the previous tile's LDS readers are done
+
+    // ---- LDS-DMA staging: 16-byte quads of every channel plane (torus-wrapped), lanes past the
+    //      region masked off (the plane pads stay zero) ----
+#pragma unroll 1
+    for (int ii_ = wave; ii_ < NI4; ii_ += NW) {
+      const int q = 64 * ii_ + lane;
+      if (q < NQ) {
+        const int e = 4 * q, vr = e / RW, vc = e - (e / RW) * RW;
+        int ii = i0 - RY + vr, jj = j0 - RX + vc;
+        ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
+        jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
+        const float* src0 = xb + ii * W + jj;
+        float* dst = xs + 256 * ii_;
+#pragma unroll 4
+        for (int c = 0; c < C; ++c)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (size_t)c * HW),
+                                           (__attribute__((address_space(3))) void*)(dst + c * PSTR), 16, 0, 0);
+      }
+    }
+    if (a.alive) {
+      // the previous K2's alive bytes over the region, one dword = 4 columns
+      const uint8_t* ab = a.alive + (size_t)b * HW;
+#pragma unroll 1
+      for (int ii_ = wave; ii_ < NIQ; ii_ += NW) {
+        const int e = 64 * ii_ + lane;
+        int off = 0;
+        if (e < NQA) {
+          const int vr = e / QW, vc = 4 * (e - (e / QW) * QW);
+          int ii = i0 - RY + vr, jj = j0 - RX + vc;
+          ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
+          jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
+          off = ii * W + jj;
+        }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ab + off),
+                                         (__attribute__((address_space(3))) void*)(al + 64 * ii_), 4, 0, 0);
+      }
+    } else {
+      // alpha plane with one more ring: element e of ((RH+2) x ALW) -> (i0-RY-1+vr, j0-RX-1+vc)
+#pragma unroll 1
+      for (int ii_ = wave; ii_ < NIA; ii_ += NW) {
+        const int e = 64 * ii_ + lane;
+        int off = 0;
+        if (e < (RH + 2) * ALW) {
+          const int vr = e / ALW, vc = e - (e / ALW) * ALW;
+          int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
+          while (ii < 0) ii += H;
+          while (ii >= H) ii -= H;
+          while (jj < 0) jj += W;
+          while (jj >= W) jj -= W;
+          off = ii * W + jj;
+        }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xb + 3 * HW + off),
+                                         (__attribute__((address_space(3))) void*)(al + 64 * ii_), 4, 0, 0);
+      }
+    }
+    // ---- fire plane while the DMA is in flight ----
+#pragma unroll 1
+    for (int n = tid; n < NCELL; n += NT) {
+      const int ti = n / TW, tj = n - (n / TW) * TW;
+      const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
+      kp[n] = fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step, a.sample_base, b, HW, cell) ? 1 : 0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // ---- sender plane over the region, keep = pre-alive AND fire over the tile ----
+    if (a.alive) {
+      const uint8_t* alb = reinterpret_cast<const uint8_t*>(al);
+#pragma unroll 1
+      for (int pos = tid; pos < RHW; pos += NT) {
+        const int vr = pos / RW, vc = pos - (pos / RW) * RW;
+        const int v = alb[pos];
+        sp[pos] = a2a ? (float)((v >> 1) & 1) : 1.f;
+        const int ti = vr - RY, tj = vc - RX;
+        if (ti >= 0 && ti < TH && tj >= 0 && tj < TW && !(v & 1)) kp[ti * TW + tj] = 0;
+      }
+    } else {
+#pragma unroll 1
+      for (int pos = tid; pos < RHW; pos += NT) {
+        const int vr = pos / RW, vc = pos - (pos / RW) * RW;
+        int iq = i0 - RY + vr, jq = j0 - RX + vc;
+        while (iq < 0) iq += H;
+        while (iq >= H) iq -= H;
+        while (jq < 0) jq += W;
+        while (jq >= W) jq -= W;
+        const float* q = al + (vr + 1) * ALW + (vc + 1);
+        const float NEG = -INFINITY;
+        const bool up = iq > 0, dn = iq < H - 1, lf = jq > 0, rt = jq < W - 1;
+        const float mu_ = fmaxf(fmaxf(lf ? q[-ALW - 1] : NEG, q[-ALW]), rt ? q[-ALW + 1] : NEG);
+        const float mm_ = fmaxf(fmaxf(lf ? q[-1] : NEG, q[0]), rt ? q[1] : NEG);
+        const float md_ = fmaxf(fmaxf(lf ? q[ALW - 1] : NEG, q[ALW]), rt ? q[ALW + 1] : NEG);
+        const float mx = fmaxf(fmaxf(up ? mu_ : NEG, mm_), dn ? md_ : NEG);
+        sp[pos] = a2a ? (mx > gthr ? 1.f : 0.f) : 1.f;
+        const int ti = vr - RY, tj = vc - RX;
+        if (ti >= 0 && ti < TH && tj >= 0 && tj < TW && !(mx > thr)) kp[ti * TW + tj] = 0;
+      }
+    }
+    __syncthreads();
+
+    // ---- live-cell compaction (cell order, wave ballots: deterministic); dead cells get dx = 0 ----
+    const size_t cell0 = (size_t)i0 * W + j0;
+    float* outb = a.out + (size_t)b * C * HW + cell0;
+    int nlive = 0;
+    for (int n0 = 0; n0 < NCELL; n0 += NT) {
+      const int n = n0 + tid;
+      const bool inb = n < NCELL;
+      const bool live = inb && kp[n] != 0;
+      const uint64_t bal = __ballot(live);
+      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) wcnt[wave] = __popcll(bal);
+      __syncthreads();
+      int off = nlive, tot = 0;
+#pragma unroll
+      for (int w_ = 0; w_ < NW; ++w_) {
+        off += w_ < wave ? wcnt[w_] : 0;
+        tot += wcnt[w_];
+      }
+      if (live) {
+        lst[off + pre] = (uint16_t)n;
+      } else if (inb) {
+        const int ti = n / TW, tj = n - (n / TW) * TW;
+        float* oz = outb + (size_t)ti * W + tj;
+#pragma unroll
+        for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
+      }
+      nlive += tot;
+      __syncthreads();   // wcnt is rewritten by the next pass
+    }
+
+    // ---- 32-cell groups ----
+    float s1 = 0.f, s2 = 0.f;
+    const int qend = (nlive + 31) >> 5;
+    const bool img_top = i0 == 0, img_bot = i0 + TH == H, img_lft = j0 == 0, img_rgt = j0 + TW == W;
+#pragma unroll 1
+    for (int q = wave; q < qend; q += NW) {
+      const int gi = 32 * q + r32;
+      const bool valid = gi < nlive;
+      const int n = lst[valid ? gi : 0];
+      const int ti = n / TW, tj = n - (n / TW) * TW;
+      const int pidx = (RY + ti) * RW + (RX + tj);
+      const int hb = 8 * h * PSTR;          // this lane's channel half
+      const int relcell = ti * W + tj;
+
+      // -- gather of alive-masked x, channels 8h..8h+7 (uniform weight 1/k, applied once) --
+      u32x4 g0 = {0u, 0u, 0u, 0u}, g1 = g0, g2 = g0;
+      float S = 0.f;
+      if constexpr (GRAPH) {
+        float gv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv[j] = 0.f;
+        const float* xq = xs + hb + pidx;
+        const float* spq = sp + pidx;
+#pragma unroll
+        for (int o = 0; o < KU; ++o) {
+          const int d = a.odl[o];
+          const float s_ = spq[-d];
+          S += s_;
+          const float* xo = xq - d;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gv[j] = fmaf(s_, xo[j * PSTR], gv[j]);
+        }
+        const float wu = a.uniform_w;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv[j] *= wu;
+        S *= wu;
+        split3_x8(gv, g0, g1, g2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+
+      // -- perception of channels 8h..8h+7 (zero padding at the image border via zero taps) --
+      float y0[8], y1[8], y2[8];
+      {
+        const int ic = i0 + ti, jc = j0 + tj;
+        const bool up = !(img_top && ic == 0), dn = !(img_bot && ic == H - 1);
+        const bool lf = !(img_lft && jc == 0), rt = !(img_rgt && jc == W - 1);
+        const int zt = RHW + hb;    // the zero tap of this lane's first channel plane
+        const int bc = pidx + hb;
+        const int t0 = (up && lf) ? bc - RW - 1 : zt, t1 = up ? bc - RW : zt, t2 = (up && rt) ? bc - RW + 1 : zt;
+        const int t3 = lf ? bc - 1 : zt, t5 = rt ? bc + 1 : zt;
+        const int t6 = (dn && lf) ? bc + RW - 1 : zt, t7 = dn ? bc + RW : zt, t8 = (dn && rt) ? bc + RW + 1 : zt;
+        if (sobel) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int co = j * PSTR;
+            const float n0 = xs[t0 + co], n1 = xs[t1 + co], n2 = xs[t2 + co];
+            const float n3 = xs[t3 + co], n4 = xs[bc + co], n5 = xs[t5 + co];
+            const float n6 = xs[t6 + co], n7 = xs[t7 + co], n8 = xs[t8 + co];
+            y0[j] = n4;
+            y1[j] = (fmaf(2.f, n3, n0) + n6) - (fmaf(2.f, n5, n2) + n8);
+            y2[j] = (fmaf(2.f, n1, n0) + n2) - (fmaf(2.f, n7, n6) + n8);
+          }
+        } else {
+#pragma unroll 1
+          for (int j = 0; j < 8; ++j) {
+            const int co = j * PSTR;
+            const float nn[9] = {xs[t0 + co], xs[t1 + co], xs[t2 + co], xs[t3 + co], xs[bc + co],
+                                 xs[t5 + co], xs[t6 + co], xs[t7 + co], xs[t8 + co]};
+            const float* pw = a.perc + (size_t)3 * (8 * h + j) * 9;
+            float acc3[3];
+#pragma unroll
+            for (int f = 0; f < 3; ++f) {
+              float acc = pw[9 * f] * nn[0];
+#pragma unroll
+              for (int t = 1; t < 9; ++t) acc = fmaf(pw[9 * f + t], nn[t], acc);
+              acc3[f] = acc;
+            }
+            y0[j] = acc3[0];
+            y1[j] = acc3[1];
+            y2[j] = acc3[2];
+          }
+        }
+      }
+      u32x4 yf[3][3];   // [kc][part]
+      split3_x8(y0, yf[0][0], yf[0][1], yf[0][2]);
+      split3_x8(y1, yf[1][0], yf[1][1], yf[1][2]);
+      split3_x8(y2, yf[2][0], yf[2][1], yf[2][2]);
+
+      // -- message: M = WM.G (stacks [M0;M1] G0 + [M2;0] G0 + [M0;M1] G1 + [M0;0] G2) --
+      f32x16 accm = {};
+      if constexpr (GRAPH) {
+        accm = mfma_bx(wmA, g0, accm);
+        accm = mfma_bx(wmB, g0, accm);
+        accm = mfma_bx(wmA, g1, accm);
+        accm = mfma_bx(wmC, g2, accm);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+
+      // -- GEMM1: H = W1.Y + b1, 4 row blocks x (bias + 3 k-chunks x 6 products) --
+      f32x16 acc[4];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const u32x4 bz = *reinterpret_cast<const u32x4*>(smem_b + L.bias + rb * 512 + r32 * 16);
+        acc[rb] = mfma_bx(bz, ones, f32x16{});
+#pragma unroll
+        for (int kc = 0; kc < 3; ++kc) {
+          const int img = L.w1 + (rb * 3 + kc) * 1024 + lane * 16;
+          const u32x4 a0 = *reinterpret_cast<const u32x4*>(smem_b + img);
+          const u32x4 a1 = *reinterpret_cast<const u32x4*>(smem_b + img + 12288);
+          const u32x4 a2 = *reinterpret_cast<const u32x4*>(smem_b + img + 24576);
+          acc[rb] = mfma_bx(a0, yf[kc][0], acc[rb]);
+          acc[rb] = mfma_bx(a0, yf[kc][1], acc[rb]);
+          acc[rb] = mfma_bx(a1, yf[kc][0], acc[rb]);
+          acc[rb] = mfma_bx(a0, yf[kc][2], acc[rb]);
+          acc[rb] = mfma_bx(a2, yf[kc][0], acc[rb]);
+          acc[rb] = mfma_bx(a1, yf[kc][1], acc[rb]);
+        }
+      }
+
+      // -- ReLU, GEMM2: DL = W2.relu(H), k-chunk s = (rb, ss) = accumulator regs 8ss..8ss+7 --
+      f32x16 accA = {}, accB = {};
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const int s = 2 * rb + ss;
+          float hv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hv[j] = relu_nan(acc[rb][8 * ss + j]);
+          u32x4 h0, h1, h2;
+          split3_x8(hv, h0, h1, h2);
+          const u32x4 T0 = *reinterpret_cast<const u32x4*>(smem_b + w2T0 + s * 512);
+          const u32x4 T1 = *reinterpret_cast<const u32x4*>(smem_b + w2T1 + s * 512);
+          accA = mfma_bx(T0, h0, accA);
+          accB = mfma_bx(T1, h0, accB);
+          accA = mfma_bx(T0, h1, accA);
+          accB = mfma_bx(T0, h2, accB);
+        }
+
+      // -- epilogue: dx = (dl + tanh(m) * gain) * keep for channels c = (r&3) + 8(r>>2) + 4h --
+      if (valid) {
+        float* ob = outb + relcell + (size_t)(4 * h) * HW;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          float v = accA[r] + accA[r + 8] + accB[r];
+          if constexpr (GRAPH) v = fmaf(fast_tanh(fmaf(bmr[r], S, accm[r] + accm[r + 8])), gainr[r], v);
+          ob[(size_t)((r & 3) + 8 * (r >> 2)) * HW] = v;
+          s1 += v;
+          s2 = fmaf(v, v, s2);
+        }
+      }
+    }
+
+    // ---- per-(tile, wave) GroupNorm partials (fp64 wave shuffle; K2 sums them in fixed order) ----
+    double d1 = s1, d2 = s2;
+    for (int off = 32; off > 0; off >>= 1) {
+      d1 += __shfl_xor(d1, off);
+      d2 += __shfl_xor(d2, off);
+    }
+    if (lane == 0) {
+      a.stats[((size_t)tile * NW + wave) * 2 + 0] = d1;
+      a.stats[((size_t)tile * NW + wave) * 2 + 1] = d2;
+    }
+  }
+}
+
+}  // namespace gnca

@@ -167,6 +167,12 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
 }
 
+}  // namespace gnca
+
+#include "gnca_k1_split.h"
+
+namespace gnca {
+
 // K1.  Template geometry (TH_, TW_, RY_, RX_) and the gather width KU_ are compile-time in the
 // specialised instantiations (every LDS offset becomes an instruction immediate); 0 = runtime.
 // fp32 MFMA shares the SIMD's fp32 datapath with VALU on gfx950 (profiles/r01_ubench_*), so the
@@ -1630,14 +1636,28 @@ struct Variant {
   const void* fn;
   int NT;                            // threads per workgroup
   int ph2;                           // 1: gnca_k1_2ph (channels staged in two phases)
+  int split;                         // 1: gnca_k1_split (bf16 MFMA on exact 3-way splits)
+  int lds_split;                     // its LDS bytes (compile-time layout)
 };
 
-#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0}
+#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0, 0}
 #define GNCA_FV(cp, hd, th, tw, ry, rx, ku, nt) \
-  {cp, hd, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, th, tw, ry, rx, ku, nt>), nt, 0}
+  {cp, hd, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, th, tw, ry, rx, ku, nt>), nt, 0, 0, 0}
 #define GNCA_2V(cp, hd, th, tw, ry, rx, ku) \
-  {cp, hd, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_2ph<cp, hd, th, tw, ry, rx, ku>), 512, 1}
+  {cp, hd, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_2ph<cp, hd, th, tw, ry, rx, ku>), 512, 1, 0, 0}
+#define GNCA_SV(th, tw, ry, rx, ku) \
+  {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), 512, 0, 1, \
+   ks_layout<th, tw, ry, rx>().total}
 static const Variant kVariants[] = {
+    // 16 channels, hidden 128, bf16 MFMA on exact 3-way splits (gnca_k1_split.h): preferred over
+    // the fp32-MFMA variants of the same shape class (GNCA_K1_F32=1 selects those instead)
+    GNCA_SV(24, 36, 4, 4, 8),
+    GNCA_SV(36, 24, 4, 4, 8),
+    GNCA_SV(24, 24, 4, 4, 8),
+    GNCA_SV(8, 24, 4, 4, 8),
+    GNCA_SV(8, 24, 1, 4, 0),     // classic NCA (no gather; RX 4 keeps the staging rows quad-aligned)
+    GNCA_SV(8, 20, 4, 4, 8),
+    GNCA_SV(8, 20, 1, 4, 0),
     // 32 channels (BASELINE config 5: 128^2, r = 5, K = 16): 16x16 tiles, channel planes staged
     // in two 16-channel phases (gnca_k1_2ph); graph and no-message steps
     GNCA_2V(32, 128, 16, 16, 5, 5, 16),
@@ -1665,6 +1685,7 @@ static const Variant kVariants[] = {
 #undef GNCA_GV
 #undef GNCA_FV
 #undef GNCA_2V
+#undef GNCA_SV
 
 static const Variant* find_variant(int C, int Hd) {
   const int CP = (C + 3) & ~3;
@@ -1718,20 +1739,23 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // measurement knobs (A/B runs only): GNCA_K1_NT256 skips the 512-thread variants,
   // GNCA_K1_TILE=<TH>x<TW> restricts the fixed variants to one tile shape
   static const bool only256 = getenv("GNCA_K1_NT256") != nullptr;
+  static const bool no_split = getenv("GNCA_K1_F32") != nullptr && atoi(getenv("GNCA_K1_F32")) != 0;
   static const char* tile_env = getenv("GNCA_K1_TILE");
   const Variant* fixed_pick = nullptr;
   long fixed_tiles = 0;
   for (const Variant& v : kVariants) {
     if (v.TH == 0 || v.CP != CP || v.HDP != HDP || d->C != CP || msg_only || attn_on) continue;
     if (only256 && v.NT > kThreads) continue;
+    if (no_split && v.split) continue;
     if (tile_env) {
       int th = 0, tw = 0;
       if (sscanf(tile_env, "%dx%d", &th, &tw) == 2 && (th != v.TH || tw != v.TW)) continue;
     }
     if (d->H % v.TH || d->W % v.TW || ry > v.RY || rx > v.RX) continue;
     if (v.KU > 0 ? !(P->graph_on && !zp && !P->need_k0 && P->k == v.KU) : P->graph_on) continue;
-    const int ltot = v.ph2 ? k1_2ph_layout(CP, HDP, v.TH, v.TW, v.RY, v.RX).total
-                           : k1_layout(CP, HDP, v.TH, v.TW, v.RY, v.RX, P->k).total;
+    const int ltot = v.split ? v.lds_split / 4
+                     : v.ph2 ? k1_2ph_layout(CP, HDP, v.TH, v.TW, v.RY, v.RX).total
+                             : k1_layout(CP, HDP, v.TH, v.TW, v.RY, v.RX, P->k).total;
     // LDS per workgroup: 80 KB for two 256-thread workgroups per CU, 160 KB for one of 512
     if ((size_t)ltot * 4 > (v.NT >= 512 ? (size_t)max_lds_bytes() : 80 * 1024)) continue;
     // list order is the large-batch preference (big tiles amortise the per-tile work); a batch
@@ -1767,8 +1791,9 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   if (P->var->TH) {
     bth = P->var->TH;
     btw = P->var->TW;
-    blds = (size_t)(P->var->ph2 ? k1_2ph_layout(CP, HDP, bth, btw, ry, rx).total
-                                : k1_layout(CP, HDP, bth, btw, ry, rx, P->k).total) * 4;
+    blds = P->var->split ? (size_t)P->var->lds_split
+                         : (size_t)(P->var->ph2 ? k1_2ph_layout(CP, HDP, bth, btw, ry, rx).total
+                                                : k1_layout(CP, HDP, bth, btw, ry, rx, P->k).total) * 4;
   }
   for (int pass = 0; pass < 2 && !bth; ++pass) {
     const size_t cap = pass == 0 ? 80 * 1024 : (size_t)max_lds_bytes();

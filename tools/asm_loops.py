@@ -21,9 +21,9 @@ blocks.append((name, cur))
 for name, ops in blocks:
     c = Counter(ops)
     tot = len(ops)
-    if tot < 15 and not c.get("v_mfma_f32_16x16x4_f32"):
+    if tot < 15 and not (c.get("v_mfma_f32_16x16x4_f32") or c.get("v_mfma_f32_32x32x16_bf16")):
         continue
-    mf = c.get("v_mfma_f32_16x16x4_f32", 0)
+    mf = c.get("v_mfma_f32_16x16x4_f32", 0) + c.get("v_mfma_f32_32x32x16_bf16", 0)
     ds = sum(v for k, v in c.items() if k.startswith("ds_"))
     vm = sum(v for k, v in c.items() if k.startswith(("global_", "flat_", "buffer_")))
     sa = sum(v for k, v in c.items() if k.startswith("s_"))
