@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import glob
 import json
 import os
 import platform
@@ -35,6 +36,7 @@ sys.path.insert(0, ROOT)
 HD, D_MODEL = 128, 16
 GAIN, THR, MSG_GAIN, FIRE = 0.05, 0.12, 0.25, 0.5
 PEAK_F32_MFMA = 157.3e12                               # MI355X_MICROARCH.md, FP32 matrix
+PEAK_BF16_MFMA = 2.5e15                                # MI355X_MICROARCH.md, BF16 dense
 PEAK_HBM = 8.0e12
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 # BASELINE.json configs as bench workloads (SURVEY.md §8d "configs restated").  "headline" is the
@@ -45,22 +47,19 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 WORKLOADS = {
     "headline": dict(graph=True, C=16, H=72, B=1024, R=4, K=8,
                      fixture="graph_torus_latest_grown_b1_72",
-                     name="graph-augmented NCA rollout, torus, r=4, K=8, fire 0.5",
-                     k1="gnca_k1_update<16,128,24,36,4,4,8,512>"),
+                     name="graph-augmented NCA rollout, torus, r=4, K=8, fire 0.5"),
     "c2": dict(graph=False, C=16, H=72, B=8, R=0, K=0, fixture="classic_ep980_b2_32",
-               name="classic NCA rollout (BASELINE config 2), fire 0.5",
-               k1="gnca_k1_update<16,128,8,24,1,1,0,512>"),
+               name="classic NCA rollout (BASELINE config 2), fire 0.5"),
     "c3": dict(graph=True, C=16, H=72, B=8, R=4, K=8, fixture="graph_torus_latest_grown_b1_72",
-               name="graph-augmented NCA rollout (BASELINE config 3), torus, r=4, K=8, fire 0.5",
-               k1="gnca_k1_update<16,128,8,24,4,4,8,512>"),
+               name="graph-augmented NCA rollout (BASELINE config 3), torus, r=4, K=8, fire 0.5"),
     "c5": dict(graph=True, C=32, H=128, B=128, R=5, K=16, fixture="graph_torus_c32_r5_k16_b1_48",
                name="graph-augmented NCA rollout (BASELINE config 5), 32ch, torus, r=5, K=16, "
-                    "fire 0.5, pool 1024 sharded 128/GPU",
-               k1="gnca_k1_2ph<32,128,16,16,5,5,16>"),
+                    "fire 0.5, pool 1024 sharded 128/GPU"),
 }
 # per-launch HBM traffic of K1/K2 measured by rocprofv3 PMC counters in separate passes
 # (tools/pmc.sh + tools/pmc_traffic.py); counters cannot be read from inside this process
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+PMC_TRAFFIC = max(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic.json")) or
+                  [os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")])
 
 
 def flop_per_cell(wl):
@@ -366,7 +365,7 @@ def main():
     B = args.batch or wl["B"]
     H = args.size or wl["H"]
     offsets_table = build_offsets(R) if graph else []
-    w, keep = weight_struct(load_weights(dev, wl), wl)
+    w, w_keep = weight_struct(load_weights(dev, wl), wl)   # w_keep owns the tensors w points at
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(B, C, H, H, device=dev, generator=g)
     x[:, 4:] = torch.randn(B, C - 4, H, H, device=dev, generator=g)
@@ -379,12 +378,14 @@ def main():
 
     rr = random.Random(42)  # same seed on every rank: identical offsets, no communication
 
-    def rollout(n, step0, src, dst):
+    def rollout(n, step0, src, dst, record=None):
         flat = []
         if graph:
             for _ in range(n):   # the per-step host draw (graph_augmentation.py:121), timed
                 for dy, dx in rr.sample(offsets_table, K):
                     flat += [dy, dx]
+        if record is not None:
+            record.extend(flat)
         arr = (ctypes.c_int8 * len(flat))(*flat) if flat else None
         d = make_desc(wl, B, H, H, offsets_table[:K], rank, step0)
         rc = lib.gnca_rollout_f32(ctypes.byref(d), ctypes.byref(w), n, arr, src.data_ptr(),
@@ -399,8 +400,9 @@ def main():
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
+    timed_offsets = []
     t0 = time.perf_counter()
-    rollout(args.steps, args.warmup, x, out)
+    rollout(args.steps, args.warmup, x, out, record=timed_offsets)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -413,53 +415,96 @@ def main():
     cells = B * H * H
     value = cells * args.steps * world / el
 
-    # --- K1 (dominant, MFMA-bound) average duration with HIP events on the launch stream, in
-    #     the rollout's mode (K1 reads the alive masks the previous K2 wrote: PHASE_ALIVE) ---
-    reps = 20
-    d = make_desc(wl, B, H, H, rr.sample(offsets_table, K) if graph else [], rank, 0)
-    L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), x.data_ptr(), out.data_ptr(),
-                                     None, None, ws.data_ptr(), ws.numel(), sptr,
-                                     L.PHASE_ALL | L.PHASE_ALIVE), "prime")
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
-    ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
-    for r in range(reps):
-        ev[2 * r].record(stream)
-        L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), out.data_ptr(),
-                                         scratch.data_ptr(), None, None, ws.data_ptr(), ws.numel(),
-                                         sptr, L.PHASE_K1 | L.PHASE_ALIVE), "k1")
-        ev[2 * r + 1].record(stream)
-        ev2[2 * r].record(stream)
-        L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), out.data_ptr(),
-                                         scratch.data_ptr(), None, None, ws.data_ptr(), ws.numel(),
-                                         sptr, L.PHASE_K2 | L.PHASE_ALIVE), "k2")
-        ev2[2 * r + 1].record(stream)
+    # --- per-kernel average durations over the timed rollout: replay it launch by launch (same
+    #     start state, offsets and fire counters, so the same work; the final state is checked
+    #     bitwise against the timed rollout's) with HIP events around every K1 and K2 launch on
+    #     the launch stream.  Step 0's K1 computes the alive masks from alpha, later K1s read the
+    #     bytes the previous K2 wrote (PHASE_ALIVE), exactly as gnca_rollout_f32 runs them. ---
+    d = make_desc(wl, B, H, H, offsets_table[:K], rank, args.warmup)
+    k1_name, arith = S.k1_variant(d)
+    tile = None
+    if arith == "bf16x6":
+        th, tw, _, _, ku = [int(v) for v in k1_name.split("<")[1].rstrip(">").split(",")]   # <TH,TW,RY,RX,KU>
+        tile = (th, tw)
+    bufs = [scratch, torch.empty_like(x)]
+    src = x
+    evs = []
+    live = torch.zeros((), dtype=torch.float64, device=dev)
+    groups = torch.zeros((), dtype=torch.int64, device=dev)
+    for t in range(args.steps):
+        o = timed_offsets[2 * K * t: 2 * K * (t + 1)]
+        d = make_desc(wl, B, H, H, [(o[2 * j], o[2 * j + 1]) for j in range(K)] if graph else [],
+                      rank, args.warmup + t)
+        dst = bufs[t % 2]
+        # this launch's live cells (keep = pre-alive AND fire: K1 runs the MLP only for them, the
+        # others have dx = 0 exactly) and, for the split K1, its padded 32-cell groups per tile
+        kp = ((torch.nn.functional.max_pool2d(src[:, 3:4], 3, 1, 1) > THR) & (S.fire_mask(d, dev) != 0))[:, 0]
+        live += kp.sum()
+        if tile:
+            per_tile = kp.reshape(B, H // tile[0], tile[0], H // tile[1], tile[1]).sum(dim=(2, 4))
+            groups += ((per_tile + 31) // 32).sum()
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        e[0].record(stream)
+        L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), src.data_ptr(), dst.data_ptr(),
+                                         None, None, ws.data_ptr(), ws.numel(), sptr,
+                                         L.PHASE_K1 | (L.PHASE_ALIVE if t > 0 else 0)), "k1")
+        e[1].record(stream)
+        e[2].record(stream)
+        L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), src.data_ptr(), dst.data_ptr(),
+                                         None, None, ws.data_ptr(), ws.numel(), sptr,
+                                         L.PHASE_K2 | L.PHASE_ALIVE), "k2")
+        e[3].record(stream)
+        evs.append(e)
+        src = dst
     torch.cuda.synchronize()
-    k1_ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(reps))[reps // 2]
-    k2_ms = sorted(ev2[2 * r].elapsed_time(ev2[2 * r + 1]) for r in range(reps))[reps // 2]
-    # live fraction of this K1 launch: cells with keep = pre-alive AND fire (the others have
-    # dx = 0 exactly and K1 skips their MLP work; the algorithmic count stays dense, per cell)
-    fm = S.fire_mask(d, dev)
-    alive = torch.nn.functional.max_pool2d(out[:, 3:4], 3, 1, 1) > THR
-    live_frac = float((alive & (fm != 0)).float().mean())
+    if not torch.equal(src.view(torch.int32), out.view(torch.int32)):
+        diff = (src != out)
+        raise SystemExit(f"bench: the launch-by-launch replay differs from the timed rollout: "
+                         f"{int(diff.sum())} values, max |d| {float((src - out).abs().nan_to_num().max()):.3e}, "
+                         f"NaN {int(src.isnan().sum())}/{int(out.isnan().sum())}")
+    k1_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)
+    k2_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / len(evs)
+    launches = args.steps
+    live_frac = float(live) / (cells * launches)
     fpc = flop_per_cell(wl)
     k1_flops = cells * fpc
     k2_bytes = cells * C * 4 * 3                   # read x, dx; write x'
     headline = args.config == "headline"
-    roof = {"bound": "mfma", "kernel": wl.get("k1", f"gnca_k1_update<{C},{HD}>"),
-            "achieved": k1_flops / (k1_ms * 1e-3) / 1e12,
-            "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
-            "frac": k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA,
+    # executed MFMA work per launch: live cells are packed into groups of 32 per tile (split K1:
+    # 108 v_mfma_f32_32x32x16_bf16 per group + 4 for the message, 32,768 FLOP each; a tile's
+    # last group is padded) or, for the f32 K1, 16,896 FLOP per live cell
+    if arith == "bf16x6":
+        exec_flops = float(groups) / launches * (112 if ku else 108) * 32768
+        peak_dtype, peak_eq = PEAK_BF16_MFMA, PEAK_BF16_MFMA / 6
+        basis = ("bf16 MFMA dense peak (2.5 PFLOP/s) / 6: K1 runs every fp32 product as 6 exact "
+                 "bf16 split products (gnca_k1_split.h)")
+    else:
+        exec_flops = float(live) / launches * fpc
+        peak_dtype = peak_eq = PEAK_F32_MFMA
+        basis = "fp32 MFMA peak (v_mfma_f32_*_f32)"
+    k1_s = k1_ms * 1e-3
+    roof = {"bound": "mfma", "kernel": k1_name, "arith": arith,
+            "achieved": k1_flops / k1_s / 1e12,
+            "peak": peak_eq / 1e12, "unit": "TFLOP/s",
+            "frac": k1_flops / k1_s / peak_eq,
+            "peak_basis": basis,
+            "vs_f32_mfma_peak": k1_flops / k1_s / PEAK_F32_MFMA,
             "traffic": pmc_traffic("K1") if headline else None,
-            "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, profiles/r01_pmc_traffic.json)",
+            "traffic_unit": f"bytes/launch (2*FETCH_SIZE+WRITE_SIZE, {os.path.relpath(PMC_TRAFFIC, ROOT)})",
             "k1_ms": k1_ms, "flop_per_launch": k1_flops,
             "live_fraction": live_frac,
-            "executed_frac": live_frac * k1_flops / (k1_ms * 1e-3) / PEAK_F32_MFMA,
-            "note": f"achieved = dense algorithmic FLOPs ({fpc:,} per cell-update, SURVEY.md 8d) / K1 "
-                    "time; K1 executes the MLP only for live cells (keep = alive AND fire, the "
-                    "others have dx = 0 exactly), so MFMA utilisation = executed_frac"}
+            "executed_mfma_tflops": exec_flops / k1_s / 1e12,
+            "mfma_busy_frac": exec_flops / k1_s / peak_dtype,
+            "k1_launches_timed": launches,
+            "note": f"achieved = dense algorithmic fp32 FLOPs ({fpc:,} per cell-update, SURVEY.md 8d) "
+                    "/ K1's average duration over the timed rollout's launches (HIP events on the "
+                    "launch stream, launch-by-launch replay).  K1 runs the MLP only for live "
+                    "cells (keep = alive AND fire; the others have dx = 0 exactly), so the MFMA "
+                    "pipe's own utilisation is mfma_busy_frac (executed MFMA FLOPs in the MFMA's "
+                    "dtype, padded groups included, / that dtype's dense peak)"}
     roof_k2 = {"bound": "hbm", "kernel": "gnca_k2_finalize", "achieved": k2_bytes / (k2_ms * 1e-3) / 1e9,
                "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": k2_bytes / (k2_ms * 1e-3) / PEAK_HBM,
-               "k2_ms": k2_ms, "bytes_per_launch": k2_bytes,
+               "k2_ms": k2_ms, "bytes_per_launch": k2_bytes, "k2_launches_timed": launches,
                "traffic": pmc_traffic("K2") if headline else None}
 
     if rank == 0:

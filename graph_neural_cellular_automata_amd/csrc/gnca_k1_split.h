@@ -155,7 +155,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
 
   // ---- weight images (bf16 parts in MFMA fragment order), once per persistent workgroup ----
-  {
+  if (!(GNCA_ABLATE & kAblFill)) {
     // W1: entry e = (rb, kc, lane): W1[32rb + (lane&31)][16kc + 8(lane>>5) + 0..7]
     for (int e = tid; e < 4 * 3 * 64; e += NT) {
       const int rb = e / 192, kc = (e / 64) % 3, l = e & 63;
@@ -252,7 +252,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
   const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
   const int t_begin = xg_ * tq + min(xg_, trm), t_end = t_begin + tq + (xg_ < trm ? 1 : 0);
-  for (int tile = t_begin + xr_; tile < t_end; tile += per_x) {
+  PROF_DECL
+  for (int tile = t_begin + xr_; tile < ((GNCA_ABLATE & kAblTiles) ? t_begin : t_end); tile += per_x) {
+    PROF_MARK(7);   // loop back-edge / tail of the previous tile
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
@@ -262,11 +264,12 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       continue;
     }
     __syncthreads();   // the previous tile's LDS readers are done
+    PROF_MARK(6);   // top barrier (waiting for the slowest wave of the previous tile)
 
     // ---- LDS-DMA staging: 16-byte quads of every channel plane (torus-wrapped), lanes past the
     //      region masked off (the plane pads stay zero) ----
 #pragma unroll 1
-    for (int ii_ = wave; ii_ < NI4; ii_ += NW) {
+    for (int ii_ = wave; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI4); ii_ += NW) {
       const int q = 64 * ii_ + lane;
       if (q < NQ) {
         const int e = 4 * q, vr = e / RW, vc = e - (e / RW) * RW;
@@ -317,21 +320,25 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
                                          (__attribute__((address_space(3))) void*)(al + 64 * ii_), 4, 0, 0);
       }
     }
+    PROF_MARK(0);   // DMA issue
     // ---- fire plane while the DMA is in flight ----
 #pragma unroll 1
     for (int n = tid; n < NCELL; n += NT) {
       const int ti = n / TW, tj = n - (n / TW) * TW;
       const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
-      kp[n] = fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step, a.sample_base, b, HW, cell) ? 1 : 0;
+      kp[n] = ((GNCA_ABLATE & kAblFire) ? ((cell & 1) != 0)
+                                        : fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step,
+                                                  a.sample_base, b, HW, cell)) ? 1 : 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    PROF_MARK(1);   // fire plane + DMA wait + barrier
 
     // ---- sender plane over the region, keep = pre-alive AND fire over the tile ----
     if (a.alive) {
       const uint8_t* alb = reinterpret_cast<const uint8_t*>(al);
 #pragma unroll 1
-      for (int pos = tid; pos < RHW; pos += NT) {
+      for (int pos = tid; pos < ((GNCA_ABLATE & kAblPlanes) ? 0 : RHW); pos += NT) {
         const int vr = pos / RW, vc = pos - (pos / RW) * RW;
         const int v = alb[pos];
         sp[pos] = a2a ? (float)((v >> 1) & 1) : 1.f;
@@ -360,6 +367,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       }
     }
     __syncthreads();
+    PROF_MARK(2);   // planes + barrier
 
     // ---- live-cell compaction (cell order, wave ballots: deterministic); dead cells get dx = 0 ----
     const size_t cell0 = (size_t)i0 * W + j0;
@@ -381,7 +389,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       }
       if (live) {
         lst[off + pre] = (uint16_t)n;
-      } else if (inb) {
+      } else if (inb && !(GNCA_ABLATE & kAblZero)) {
         const int ti = n / TW, tj = n - (n / TW) * TW;
         float* oz = outb + (size_t)ti * W + tj;
 #pragma unroll
@@ -390,6 +398,8 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       nlive += tot;
       __syncthreads();   // wcnt is rewritten by the next pass
     }
+
+    PROF_MARK(3);   // compaction
 
     // ---- 32-cell groups ----
     float s1 = 0.f, s2 = 0.f;
@@ -408,7 +418,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       // -- gather of alive-masked x, channels 8h..8h+7 (uniform weight 1/k, applied once) --
       u32x4 g0 = {0u, 0u, 0u, 0u}, g1 = g0, g2 = g0;
       float S = 0.f;
-      if constexpr (GRAPH) {
+      if constexpr (GRAPH) if (!(GNCA_ABLATE & kAblGather)) {
         float gv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) gv[j] = 0.f;
@@ -442,7 +452,10 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
         const int t0 = (up && lf) ? bc - RW - 1 : zt, t1 = up ? bc - RW : zt, t2 = (up && rt) ? bc - RW + 1 : zt;
         const int t3 = lf ? bc - 1 : zt, t5 = rt ? bc + 1 : zt;
         const int t6 = (dn && lf) ? bc + RW - 1 : zt, t7 = dn ? bc + RW : zt, t8 = (dn && rt) ? bc + RW + 1 : zt;
-        if (sobel) {
+        if (GNCA_ABLATE & kAblPerceive) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y0[j] = y1[j] = y2[j] = 0.f;
+        } else if (sobel) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const int co = j * PSTR;
@@ -478,10 +491,14 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       split3_x8(y0, yf[0][0], yf[0][1], yf[0][2]);
       split3_x8(y1, yf[1][0], yf[1][1], yf[1][2]);
       split3_x8(y2, yf[2][0], yf[2][1], yf[2][2]);
+      if (GNCA_ABLATE & kAblMfma) {
+#pragma unroll
+        for (int kc = 0; kc < 3; ++kc) asm volatile("" ::"v"(yf[kc][0]), "v"(yf[kc][1]), "v"(yf[kc][2]));
+      }
 
       // -- message: M = WM.G (stacks [M0;M1] G0 + [M2;0] G0 + [M0;M1] G1 + [M0;0] G2) --
       f32x16 accm = {};
-      if constexpr (GRAPH) {
+      if constexpr (GRAPH) if (!(GNCA_ABLATE & kAblMfma)) {
         accm = mfma_bx(wmA, g0, accm);
         accm = mfma_bx(wmB, g0, accm);
         accm = mfma_bx(wmA, g1, accm);
@@ -489,11 +506,16 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       }
       __builtin_amdgcn_sched_barrier(0);
 
+      f32x16 accA = {}, accB = {};
       // -- GEMM1: H = W1.Y + b1, 4 row blocks x (bias + 3 k-chunks x 6 products) --
       f32x16 acc[4];
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         const u32x4 bz = *reinterpret_cast<const u32x4*>(smem_b + L.bias + rb * 512 + r32 * 16);
+        if (GNCA_ABLATE & kAblMfma) {
+          acc[rb] = f32x16{};
+          continue;
+        }
         acc[rb] = mfma_bx(bz, ones, f32x16{});
 #pragma unroll
         for (int kc = 0; kc < 3; ++kc) {
@@ -511,7 +533,6 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       }
 
       // -- ReLU, GEMM2: DL = W2.relu(H), k-chunk s = (rb, ss) = accumulator regs 8ss..8ss+7 --
-      f32x16 accA = {}, accB = {};
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
@@ -522,6 +543,10 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
           for (int j = 0; j < 8; ++j) hv[j] = relu_nan(acc[rb][8 * ss + j]);
           u32x4 h0, h1, h2;
           split3_x8(hv, h0, h1, h2);
+          if (GNCA_ABLATE & kAblMfma) {
+            asm volatile("" ::"v"(h0), "v"(h1), "v"(h2));
+            continue;
+          }
           const u32x4 T0 = *reinterpret_cast<const u32x4*>(smem_b + w2T0 + s * 512);
           const u32x4 T1 = *reinterpret_cast<const u32x4*>(smem_b + w2T1 + s * 512);
           accA = mfma_bx(T0, h0, accA);
@@ -537,14 +562,17 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
         for (int r = 0; r < 8; ++r) {
           float v = accA[r] + accA[r + 8] + accB[r];
           if constexpr (GRAPH) v = fmaf(fast_tanh(fmaf(bmr[r], S, accm[r] + accm[r + 8])), gainr[r], v);
-          ob[(size_t)((r & 3) + 8 * (r >> 2)) * HW] = v;
+          if (GNCA_ABLATE & kAblStore) asm volatile("" ::"v"(v));
+          else ob[(size_t)((r & 3) + 8 * (r >> 2)) * HW] = v;
           s1 += v;
           s2 = fmaf(v, v, s2);
         }
       }
     }
 
+    PROF_MARK(4);   // group loop
     // ---- per-(tile, wave) GroupNorm partials (fp64 wave shuffle; K2 sums them in fixed order) ----
+    if (GNCA_ABLATE & kAblReduce) continue;
     double d1 = s1, d2 = s2;
     for (int off = 32; off > 0; off >>= 1) {
       d1 += __shfl_xor(d1, off);
@@ -554,7 +582,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       a.stats[((size_t)tile * NW + wave) * 2 + 0] = d1;
       a.stats[((size_t)tile * NW + wave) * 2 + 1] = d2;
     }
+    PROF_MARK(5);   // per-tile reduction
   }
+  PROF_STORE_W04;
 }
 
 }  // namespace gnca

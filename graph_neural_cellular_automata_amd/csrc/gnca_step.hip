@@ -69,7 +69,10 @@ __device__ unsigned long long g_prof[1024][2 * kProfPhases];   // [.][8..15]: sp
 #define PROF_DECL unsigned long long prof_t = __builtin_amdgcn_s_memtime(), prof_acc[kProfPhases] = {0};
 #define PROF_MARK(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
 #define PROF_STORE do { if (threadIdx.x == 0) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][i_] = prof_acc[i_]; } while (0)
+// waves 0 and 4 (the two waves of SIMD 0): [.][0..7] and [.][8..15]
+#define PROF_STORE_W04 do { if ((threadIdx.x & 255) == 0) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][(threadIdx.x >> 8) * kProfPhases + i_] = prof_acc[i_]; } while (0)
 #else
+#define PROF_STORE_W04 do {} while (0)
 #define PROF_DECL
 #define PROF_MARK(i) do {} while (0)
 #define PROF_STORE do {} while (0)
@@ -2082,6 +2085,21 @@ size_t gnca_workspace_bytes(const gnca_step_desc* desc) {
   size_t m = P.ws_bytes;
   if ((desc->flags & GNCA_GRAPH) && make_plan(desc, true, &Q) && Q.ws_bytes > m) m = Q.ws_bytes;
   return m;
+}
+
+int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* arith) {
+  Plan P;
+  if (!name || n <= 0 || !make_plan(desc, false, &P)) return GNCA_ERR_INVALID;
+  const Variant* v = P.var;
+  if (v->split)
+    snprintf(name, (size_t)n, "gnca_k1_split<%d,%d,%d,%d,%d>", v->TH, v->TW, v->RY, v->RX, v->KU);
+  else if (v->ph2)
+    snprintf(name, (size_t)n, "gnca_k1_2ph<%d,%d,%d,%d,%d,%d,%d>", v->CP, v->HDP, v->TH, v->TW, v->RY, v->RX, v->KU);
+  else
+    snprintf(name, (size_t)n, "gnca_k1_update<%d,%d,%d,%d,%d,%d,%d,%d>", v->CP, v->HDP, v->TH, v->TW, v->RY, v->RX,
+             v->KU, v->NT);
+  if (arith) *arith = v->split ? 1 : 0;
+  return GNCA_OK;
 }
 
 int gnca_step_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x, float* x_out,

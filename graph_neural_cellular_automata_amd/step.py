@@ -86,6 +86,15 @@ def workspace(desc: L.StepDesc, device) -> torch.Tensor:
     return torch.empty(n, dtype=torch.uint8, device=device)
 
 
+def k1_variant(desc: L.StepDesc) -> tuple[str, str]:
+    """(kernel name, MFMA arithmetic) of the K1 the plan for ``desc`` launches: arithmetic "f32"
+    (fp32 MFMA) or "bf16x6" (bf16 MFMA on exact 3-way splits, 6 products per fp32 product)."""
+    buf = ctypes.create_string_buffer(128)
+    arith = ctypes.c_int32(0)
+    L.check(L.load().gnca_k1_variant(ctypes.byref(desc), buf, 128, ctypes.byref(arith)), "gnca_k1_variant")
+    return buf.value.decode(), ("bf16x6" if arith.value == 1 else "f32")
+
+
 def stream_ptr(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 

@@ -115,6 +115,12 @@ int gnca_last_hip_error(void);
 /* Bytes of device workspace gnca_step_f32 needs for `desc` (0 on invalid desc). */
 size_t gnca_workspace_bytes(const gnca_step_desc* desc);
 
+/* Measurement: the K1 kernel the plan for `desc` launches, as "name<template args>" (NUL-terminated,
+ * truncated to n bytes), and its MFMA arithmetic in *arith (may be NULL): 0 = fp32 MFMA
+ * (v_mfma_f32_*_f32), 1 = bf16 MFMA on exact 3-way splits of the fp32 operands (6 products per
+ * fp32 product, gnca_k1_split.h).  Host-only.  Returns GNCA_OK or GNCA_ERR_INVALID. */
+int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* arith);
+
 /*
  * One CA step: x_out = step(x).  Out-of-place (x_out must not alias x), like the reference.
  *   fire:  NULL, or [B,1,H,W] fp32 uniforms (GNCA_FIRE_RAND_F32) / uint8 mask (GNCA_FIRE_MASK_U8)

@@ -22,6 +22,9 @@ VARIANTS = {
 }
 
 
+# experiment builds: ABLATE_EXTRA="name=-DFOO=1 -DBAR;name2=-DBAZ" (each built and timed beside the others)
+EXTRA = dict(e.split("=", 1) for e in os.environ.get("ABLATE_EXTRA", "").split(";") if "=" in e)
+VARIANTS.update({n: f for n, f in EXTRA.items()})
 ONLY = [v for v in os.environ.get("ABLATE_ONLY", "").split(",") if v]   # e.g. "full,prof"
 CONFIG = os.environ.get("ABLATE_CONFIG", "headline")                    # a bench.py WORKLOADS key
 
@@ -33,7 +36,8 @@ def build():
     for name, bits in list(VARIANTS.items()) + [("prof", None)]:
         if ONLY and name not in ONLY:
             continue
-        flags = ["-DGNCA_PROFILE"] if bits is None else [f"-DGNCA_ABLATE={bits}"]
+        flags = (["-DGNCA_PROFILE"] if bits is None else
+                 bits.split() if isinstance(bits, str) else [f"-DGNCA_ABLATE={bits}"])
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                *flags, f"-I{ROOT}/include", src, "-o", os.path.join(OUT, f"lib_{name}.so")]
         procs.append(subprocess.Popen(cmd, stderr=subprocess.DEVNULL))
@@ -93,6 +97,8 @@ def run(reps=15, rounds=3):
     for n, v in res.items():
         v.sort()
         print(f"{n:18s} median {v[len(v)//2]:.3f} ms   min {v[0]:.3f} ms")
+    if ONLY and "prof" not in ONLY:
+        return
     # phase timers of the profile build (s_memtime cycles summed over each workgroup's tiles)
     pl = ctypes.CDLL(os.path.join(OUT, "lib_prof.so"))
     pl.gnca_step_phases_f32.restype = ctypes.c_int
@@ -108,7 +114,12 @@ def run(reps=15, rounds=3):
     import numpy as np
     full = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16).astype(np.float64)
     ws = full[:, 8:].sum() > 0
-    if ws:
+    if os.environ.get("ABLATE_PROF_SETS") == "w04":   # the split K1: both waves of SIMD 0
+        names = ["dma_issue", "fire+dma_wait", "planes", "compaction", "groups", "reduction",
+                 "top_barrier", "loop_tail"]
+        sets = [("wave 0 (SIMD 0, older)", names, full[:, :8]),
+                ("wave 4 (SIMD 0, younger)", names, full[:, 8:])]
+    elif ws:
         sets = [("producer wave 0", ["dma_issue", "fire+dma_wait+pbar", "planes+pbar", "compaction",
                                      "y_compute", "wait_empty", "end_tile_pbar", "end_stream"], full[:, :8]),
                 ("consumer wave 4", ["wait_full", "compute", "read+flush", "-", "-", "-", "-", "-"], full[:, 8:])]
