@@ -95,7 +95,7 @@ __host__ __device__ constexpr int ks_pstr(int rhw) {
 }
 
 struct KSLayout {
-  int xs, sp, al, kp, lst, wcnt, red, w1, bias, w2, wm, wz, total;   // byte offsets
+  int xs, sp, al, kp, lst, wcnt, red, w1, bias, w2, wm, wz, bml, total;   // byte offsets
 };
 
 __host__ __device__ constexpr int ks_a16(int v) { return (v + 15) & ~15; }
@@ -119,6 +119,7 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   L.w2 = o; o += 3 * 8 * 2 * 16 * 16;    // [plane][s][h][channel] x 16 B
   L.wm = o; o += 3 * 2 * 16 * 16;        // [plane][h][channel] x 16 B
   L.wz = o; o += 2 * 16 * 16;            // zeros, laid out like one WM plane
+  L.bml = o; o += 2 * 8 * 4;             // message bias per (lane half h, accumulator register r)
   L.total = o;
   return L;
 }
@@ -207,6 +208,11 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       *reinterpret_cast<u32x4*>(smem_b + L.wm + 2 * 512 + e * 16) = f2;
     }
     for (int e = tid; e < 32; e += NT) *reinterpret_cast<u32x4*>(smem_b + L.wz + e * 16) = u32x4{0u, 0u, 0u, 0u};
+    // message bias of output channel c = (r&3) + 8(r>>2) + 4h at [h][r]
+    if (tid < 16) {
+      const int hh = tid >> 3, r = tid & 7;
+      reinterpret_cast<float*>(smem_b + L.bml)[tid] = GRAPH ? a.bm[(r & 3) + 8 * (r >> 2) + 4 * hh] : 0.f;
+    }
     // the perception zero tap: every channel plane's pad floats (never written by the staging)
     for (int e = tid; e < 16 * (PSTR - RHW); e += NT) xs[(e / (PSTR - RHW)) * PSTR + RHW + e % (PSTR - RHW)] = 0.f;
   }
@@ -223,23 +229,18 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   }
   const bool sobel = __syncthreads_and(ok) != 0;   // also the barrier after the image stores
 
-  // per-lane constants: message fragments (stacks [M0;M1], [M2;0], [M0;0]), ones for the bias,
-  // message bias / gain of this lane's 8 output channels c = (r&3) + 8(r>>2) + 4h
-  u32x4 wmA = {0u, 0u, 0u, 0u}, wmB = wmA, wmC = wmA;
-  if (GRAPH) {
-    const int ent = (h * 16 + c16) * 16;
-    wmA = *reinterpret_cast<const u32x4*>(smem_b + L.wm + (r32 < 16 ? 0 : 512) + ent);
-    wmB = *reinterpret_cast<const u32x4*>(smem_b + (r32 < 16 ? L.wm + 1024 : L.wz) + ent);
-    wmC = *reinterpret_cast<const u32x4*>(smem_b + (r32 < 16 ? L.wm : L.wz) + ent);
-  }
+  // per-lane LDS offsets of the message fragments (stacks [M0;M1], [M2;0], [M0;0], read per
+  // group: kept out of the registers the group loop needs) and of the message bias of this lane's 8
+  // output channels c = (r&3) + 8(r>>2) + 4h; ones for the bias MFMA
+  const int ent_ = (h * 16 + c16) * 16;
+  const int wmA_o = L.wm + (r32 < 16 ? 0 : 512) + ent_;
+  const int wmB_o = (r32 < 16 ? L.wm + 1024 : L.wz) + ent_;
+  const int wmC_o = (r32 < 16 ? L.wm : L.wz) + ent_;
+  const int bml_o = L.bml + h * 32;
   const u32x4 ones = h == 0 ? u32x4{0x3f803f80u, 0x3f80u, 0u, 0u} : u32x4{0u, 0u, 0u, 0u};
-  float bmr[8], gainr[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int c = (r & 3) + 8 * (r >> 2) + 4 * h;
-    bmr[r] = GRAPH ? a.bm[c] : 0.f;
-    gainr[r] = (GRAPH && !(hidden_only && c < 4)) ? a.message_gain : 0.f;
-  }
+  // message gain: 0 for the RGBA channels (c < 4: h == 0, r < 4) under hidden_only
+  const float mgain = GRAPH ? a.message_gain : 0.f;
+  const bool hz = hidden_only && h == 0;
   // W2 A-fragment lane bases: T0 = [P0;P1], T1 = [P2;P2] (+ s * 512 per k-chunk)
   const int w2T0 = L.w2 + (r32 < 16 ? 0 : 4096) + (h * 16 + c16) * 16;
   const int w2T1 = L.w2 + 8192 + (h * 16 + c16) * 16;
@@ -499,6 +500,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       // -- message: M = WM.G (stacks [M0;M1] G0 + [M2;0] G0 + [M0;M1] G1 + [M0;0] G2) --
       f32x16 accm = {};
       if constexpr (GRAPH) if (!(GNCA_ABLATE & kAblMfma)) {
+        const u32x4 wmA = *reinterpret_cast<const u32x4*>(smem_b + wmA_o);
+        const u32x4 wmB = *reinterpret_cast<const u32x4*>(smem_b + wmB_o);
+        const u32x4 wmC = *reinterpret_cast<const u32x4*>(smem_b + wmC_o);
         accm = mfma_bx(wmA, g0, accm);
         accm = mfma_bx(wmB, g0, accm);
         accm = mfma_bx(wmA, g1, accm);
@@ -561,7 +565,10 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           float v = accA[r] + accA[r + 8] + accB[r];
-          if constexpr (GRAPH) v = fmaf(fast_tanh(fmaf(bmr[r], S, accm[r] + accm[r + 8])), gainr[r], v);
+          if constexpr (GRAPH) {
+            const float bm_ = reinterpret_cast<const float*>(smem_b + bml_o)[r];
+            v = fmaf(fast_tanh(fmaf(bm_, S, accm[r] + accm[r + 8])), (hz && r < 4) ? 0.f : mgain, v);
+          }
           if (GNCA_ABLATE & kAblStore) asm volatile("" ::"v"(v));
           else ob[(size_t)((r & 3) + 8 * (r >> 2)) * HW] = v;
           s1 += v;
