@@ -470,11 +470,13 @@ def main():
     k1_flops = cells * fpc
     k2_bytes = cells * C * 4 * 3                   # read x, dx; write x'
     headline = args.config == "headline"
-    # executed MFMA work per launch: live cells are packed into groups of 32 per tile (split K1:
-    # 108 v_mfma_f32_32x32x16_bf16 per group + 4 for the message, 32,768 FLOP each; a tile's
-    # last group is padded) or, for the f32 K1, 16,896 FLOP per live cell
+    # executed MFMA work per launch: live cells are packed into groups of 32 per tile (split K1,
+    # v_mfma_f32_32x32x16_bf16 of 32,768 FLOP each per group: 16 channels 108 + 4 for the message,
+    # 32 channels 196 + 12; a tile's last group is padded) or, for the f32 K1, the dense FLOPs per
+    # live cell
     if arith == "bf16x6":
-        exec_flops = float(groups) / launches * (112 if ku else 108) * 32768
+        per_group = (112 if ku else 108) if C == 16 else (208 if ku else 196)
+        exec_flops = float(groups) / launches * per_group * 32768
         peak_dtype, peak_eq = PEAK_BF16_MFMA, PEAK_BF16_MFMA / 6
         basis = ("bf16 MFMA dense peak (2.5 PFLOP/s) / 6: K1 runs every fp32 product as 6 exact "
                  "bf16 split products (gnca_k1_split.h)")

@@ -439,6 +439,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
         for (int j = 0; j < 8; ++j) gv[j] *= wu;
         S *= wu;
         split3_x8(gv, g0, g1, g2);
+        // materialise here (before the perception's sobel / generic branch): otherwise the
+        // gather arithmetic is sunk past the branch and its loaded floats stay live longer
+        asm volatile("" : "+v"(g0), "+v"(g1), "+v"(g2), "+v"(S));
       }
       __builtin_amdgcn_sched_barrier(0);
 

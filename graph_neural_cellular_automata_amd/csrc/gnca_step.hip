@@ -173,6 +173,7 @@ __device__ __forceinline__ float fast_tanh(float x) {
 }  // namespace gnca
 
 #include "gnca_k1_split.h"
+#include "gnca_k1_split32.h"
 
 namespace gnca {
 
@@ -1652,7 +1653,7 @@ struct Variant {
   const void* fn;
   int NT;                            // threads per workgroup
   int ph2;                           // 1: gnca_k1_2ph (channels staged in two phases)
-  int split;                         // 1: gnca_k1_split (bf16 MFMA on exact 3-way splits)
+  int split;                         // 1: gnca_k1_split, 2: gnca_k1_split32 (bf16 MFMA on exact 3-way splits)
   int lds_split;                     // its LDS bytes (compile-time layout)
 };
 
@@ -1664,6 +1665,9 @@ struct Variant {
 #define GNCA_SV(th, tw, ry, rx, ku) \
   {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), 512, 0, 1, \
    ks_layout<th, tw, ry, rx>().total}
+#define GNCA_S32V(th, tw, ry, rx, ku) \
+  {32, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split32<th, tw, ry, rx, ku>), 512, 0, 2, \
+   ks32_layout<th, tw, ry, rx>().total}
 static const Variant kVariants[] = {
     // 16 channels, hidden 128, bf16 MFMA on exact 3-way splits (gnca_k1_split.h): preferred over
     // the fp32-MFMA variants of the same shape class (GNCA_K1_F32=1 selects those instead)
@@ -1675,7 +1679,10 @@ static const Variant kVariants[] = {
     GNCA_SV(8, 20, 4, 4, 8),
     GNCA_SV(8, 20, 1, 4, 0),
     // 32 channels (BASELINE config 5: 128^2, r = 5, K = 16): 16x16 tiles, channel planes staged
-    // in two 16-channel phases (gnca_k1_2ph); graph and no-message steps
+    // in two 16-channel phases; bf16 split MFMA (gnca_k1_split32.h), then the fp32-MFMA
+    // gnca_k1_2ph (GNCA_K1_F32=1); graph and no-message steps
+    GNCA_S32V(16, 16, 5, 5, 16),
+    GNCA_S32V(16, 16, 1, 1, 0),
     GNCA_2V(32, 128, 16, 16, 5, 5, 16),
     GNCA_2V(32, 128, 16, 16, 1, 1, 0),
     // compile-time geometry: the benchmark / trainer shapes (16 ch, hidden 128, 8x24 tiles)
@@ -1702,6 +1709,7 @@ static const Variant kVariants[] = {
 #undef GNCA_FV
 #undef GNCA_2V
 #undef GNCA_SV
+#undef GNCA_S32V
 
 static const Variant* find_variant(int C, int Hd) {
   const int CP = (C + 3) & ~3;
@@ -2109,7 +2117,8 @@ int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* 
   if (!name || n <= 0 || !make_plan(desc, false, &P)) return GNCA_ERR_INVALID;
   const Variant* v = P.var;
   if (v->split)
-    snprintf(name, (size_t)n, "gnca_k1_split<%d,%d,%d,%d,%d>", v->TH, v->TW, v->RY, v->RX, v->KU);
+    snprintf(name, (size_t)n, "gnca_k1_split%s<%d,%d,%d,%d,%d>", v->split == 2 ? "32" : "", v->TH, v->TW, v->RY,
+             v->RX, v->KU);
   else if (v->ph2)
     snprintf(name, (size_t)n, "gnca_k1_2ph<%d,%d,%d,%d,%d,%d,%d>", v->CP, v->HDP, v->TH, v->TW, v->RY, v->RX, v->KU);
   else
