@@ -432,7 +432,12 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
           S += s_;
           const float* xo = xq - d;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) gv[j] = fmaf(s_, xo[j * PSTR], gv[j]);
+          for (int j = 0; j < 8; ++j) {
+            // (GNCA_ABLATE & 4096: timing only, one channel's read stands in for all eight)
+            float xv_ = xo[(GNCA_ABLATE & 4096) ? 0 : j * PSTR];
+            if (GNCA_ABLATE & 4096) asm volatile("" : "+v"(xv_));
+            gv[j] = fmaf(s_, xv_, gv[j]);
+          }
         }
         const float wu = a.uniform_w;
 #pragma unroll
@@ -462,10 +467,12 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
         } else if (sobel) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const int co = j * PSTR;
-            const float n0 = xs[t0 + co], n1 = xs[t1 + co], n2 = xs[t2 + co];
-            const float n3 = xs[t3 + co], n4 = xs[bc + co], n5 = xs[t5 + co];
-            const float n6 = xs[t6 + co], n7 = xs[t7 + co], n8 = xs[t8 + co];
+            const int co = (GNCA_ABLATE & 4096) ? 0 : j * PSTR;
+            float n0 = xs[t0 + co], n1 = xs[t1 + co], n2 = xs[t2 + co];
+            float n3 = xs[t3 + co], n4 = xs[bc + co], n5 = xs[t5 + co];
+            float n6 = xs[t6 + co], n7 = xs[t7 + co], n8 = xs[t8 + co];
+            if (GNCA_ABLATE & 4096)
+              asm volatile("" : "+v"(n0), "+v"(n1), "+v"(n2), "+v"(n3), "+v"(n4), "+v"(n5), "+v"(n6), "+v"(n7), "+v"(n8));
             y0[j] = n4;
             y1[j] = (fmaf(2.f, n3, n0) + n6) - (fmaf(2.f, n5, n2) + n8);
             y2[j] = (fmaf(2.f, n1, n0) + n2) - (fmaf(2.f, n7, n6) + n8);

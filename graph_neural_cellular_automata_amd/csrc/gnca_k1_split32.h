@@ -176,7 +176,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     // channel planes [16ph, 16ph + 16) of the (RH x RW) region -> xs (torus-wrapped), dword DMA
     auto stage = [&](int ph) {
 #pragma unroll 1
-      for (int ii_ = wave; ii_ < NI; ii_ += NW) {
+      for (int ii_ = wave; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI); ii_ += NW) {
         const int e = 64 * ii_ + lane;
         if (e < RHW) {   // lanes past the region masked off: the plane pads (zero taps) stay zero
           const int vr = e / RW, vc = e - (e / RW) * RW;
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       if (!has) continue;
       // -- gather of alive-masked x, this phase's channels 16ph + 8h + j (uniform weight 1/k) --
       u32x4 g0 = {0u, 0u, 0u, 0u}, g1 = g0, g2 = g0;
-      if constexpr (GRAPH) {
+      if constexpr (GRAPH) if (!(GNCA_ABLATE & kAblGather)) {
         float gv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) gv[j] = 0.f;
@@ -369,7 +369,10 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       const int t0 = (up && lf) ? bc - RW - 1 : zt, t1 = up ? bc - RW : zt, t2 = (up && rt) ? bc - RW + 1 : zt;
       const int t3 = lf ? bc - 1 : zt, t5 = rt ? bc + 1 : zt;
       const int t6 = (dn && lf) ? bc + RW - 1 : zt, t7 = dn ? bc + RW : zt, t8 = (dn && rt) ? bc + RW + 1 : zt;
-      if (sobel) {
+      if (GNCA_ABLATE & kAblPerceive) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y0[j] = y1[j] = y2[j] = 0.f;
+      } else if (sobel) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int co = j * PSTR;
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     }
 
     float s1 = 0.f, s2 = 0.f;
-    if (has) {
+    if (has && !(GNCA_ABLATE & kAblMfma)) {
       // -- message: chunks p = 0, 1, 6 products each --
       f32x16 accm = {};
       if constexpr (GRAPH) {
