@@ -125,3 +125,27 @@ def test_bwd_rejects_bad_args_without_touching_gpu(lib):
     rc2 = lib.gnca_step_masked_f32(ctypes.byref(d), ctypes.byref(w), None, None, None, None, None, 0, None)
     assert rc2 == -1
     assert rc == -1
+
+
+def test_k1_variant_names(lib):
+    """gnca_k1_variant (host-only) names the K1 each BASELINE workload shape plans: the bf16-split
+    kernels for 16 and 32 channels, the fp32-MFMA kernel for other shape classes."""
+    from graph_neural_cellular_automata_amd import _lib as L_
+    flags = L_.USE_GROUPNORM | L_.GRAPH | L_.HIDDEN_ONLY | L_.ALIVE_TO_ALIVE
+
+    def name(B, C, H, offs, hidden=128, graph=True):
+        d = S.make_desc(B=B, C=C, H=H, W=H, hidden=hidden, d_model=16, offsets=offs,
+                        flags=flags if graph else L_.USE_GROUPNORM, update_gain=0.05, alpha_thr=0.12,
+                        message_gain=0.25, fire_rate=0.5, fire_mode=L_.FIRE_HASH)
+        return S.k1_variant(d)
+
+    r4 = [(dy, dx) for dy in range(-4, 5) for dx in range(-4, 5) if max(abs(dy), abs(dx)) > 1][:8]
+    r5 = [(dy, dx) for dy in range(-5, 6) for dx in range(-5, 6) if max(abs(dy), abs(dx)) > 1][:16]
+    assert name(1024, 16, 72, r4) == ("gnca_k1_split<24,36,4,4,8>", "bf16x6")
+    assert name(8, 16, 72, r4) == ("gnca_k1_split<8,24,4,4,8>", "bf16x6")
+    assert name(8, 16, 72, [], graph=False) == ("gnca_k1_split<8,24,1,4,0>", "bf16x6")
+    assert name(128, 32, 128, r5) == ("gnca_k1_split32<16,16,5,5,16>", "bf16x6")
+    nm, ar = name(4, 12, 20, r4, hidden=64)
+    assert nm.startswith("gnca_k1_update<12,64,") and ar == "f32"
+    buf = ctypes.create_string_buffer(8)
+    assert lib.gnca_k1_variant(None, buf, 8, None) != 0
