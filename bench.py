@@ -447,12 +447,12 @@ def main():
         e[0].record(stream)
         L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), src.data_ptr(), dst.data_ptr(),
                                          None, None, ws.data_ptr(), ws.numel(), sptr,
-                                         L.PHASE_K1 | (L.PHASE_ALIVE if t > 0 else 0)), "k1")
+                                         L.PHASE_K1 | L.PHASE_COMPACT | (L.PHASE_ALIVE if t > 0 else 0)), "k1")
         e[1].record(stream)
         e[2].record(stream)
         L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), src.data_ptr(), dst.data_ptr(),
                                          None, None, ws.data_ptr(), ws.numel(), sptr,
-                                         L.PHASE_K2 | L.PHASE_ALIVE), "k2")
+                                         L.PHASE_K2 | L.PHASE_COMPACT | L.PHASE_ALIVE), "k2")
         e[3].record(stream)
         evs.append(e)
         src = dst
@@ -468,7 +468,9 @@ def main():
     live_frac = float(live) / (cells * launches)
     fpc = flop_per_cell(wl)
     k1_flops = cells * fpc
-    k2_bytes = cells * C * 4 * 3                   # read x, dx; write x'
+    compact = S.rollout_compact(d)
+    # read x, write x'; read dx: dense NCHW, or on the compact field only the live cells' values
+    k2_bytes = cells * C * 4 * (2 + (live_frac if compact else 1.0))
     headline = args.config == "headline"
     # executed MFMA work per launch: live cells are packed into groups of 32 per tile (split K1,
     # v_mfma_f32_32x32x16_bf16 of 32,768 FLOP each per group: 16 channels 108 + 4 for the message,
@@ -504,7 +506,8 @@ def main():
                     "cells (keep = alive AND fire; the others have dx = 0 exactly), so the MFMA "
                     "pipe's own utilisation is mfma_busy_frac (executed MFMA FLOPs in the MFMA's "
                     "dtype, padded groups included, / that dtype's dense peak)"}
-    roof_k2 = {"bound": "hbm", "kernel": "gnca_k2_finalize", "achieved": k2_bytes / (k2_ms * 1e-3) / 1e9,
+    roof_k2 = {"bound": "hbm", "kernel": "gnca_k2_finalize", "update_field": "compact" if compact else "dense",
+               "achieved": k2_bytes / (k2_ms * 1e-3) / 1e9,
                "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": k2_bytes / (k2_ms * 1e-3) / PEAK_HBM,
                "k2_ms": k2_ms, "bytes_per_launch": k2_bytes, "k2_launches_timed": launches,
                "traffic": pmc_traffic("K2") if headline else None}

@@ -12,7 +12,8 @@ import os
 import torch  # noqa: F401  — load torch's HIP runtime first; libgnca.so binds to it by soname
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgnca.so")
+# GNCA_LIB_PATH: an alternative build of the same library (A/B measurement runs only)
+LIB_PATH = os.environ.get("GNCA_LIB_PATH") or os.path.join(_HERE, "libgnca.so")
 
 ABI_VERSION = 2
 MAX_OFFSETS = 128
@@ -76,6 +77,7 @@ EXPORTS = ("gnca_abi_version", "gnca_status_string", "gnca_last_hip_error",
 PHASE_K0, PHASE_K1, PHASE_K2 = 1, 2, 4
 PHASE_ALL = 7
 PHASE_ALIVE = 8   # rollout mode: K2 hands the next step's alive masks to K1 (include/gnca.h)
+PHASE_COMPACT = 16   # rollout mode: K1 packs the live cells' dx per tile, K2 unpacks (include/gnca.h)
 
 _lib = None
 

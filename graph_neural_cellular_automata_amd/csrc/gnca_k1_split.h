@@ -154,6 +154,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
+  const bool compact = a.rmask != nullptr;
+  static_assert(TW <= 64, "one ballot per tile row (compact update field)");
+  auto tj0 = [](int n) { return n - (n / TW) * TW; };
 
   // ---- weight images (bf16 parts in MFMA fragment order), once per persistent workgroup ----
   if (!(GNCA_ABLATE & kAblFill)) {
@@ -388,9 +391,10 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
         off += w_ < wave ? wcnt[w_] : 0;
         tot += wcnt[w_];
       }
+      if (compact && inb && tj0(n) == 0) a.rpre[(size_t)tile * TH + n / TW] = (uint32_t)(off + pre);
       if (live) {
         lst[off + pre] = (uint16_t)n;
-      } else if (inb && !(GNCA_ABLATE & kAblZero)) {
+      } else if (inb && !compact && !(GNCA_ABLATE & kAblZero)) {
         const int ti = n / TW, tj = n - (n / TW) * TW;
         float* oz = outb + (size_t)ti * W + tj;
 #pragma unroll
@@ -400,6 +404,13 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       __syncthreads();   // wcnt is rewritten by the next pass
     }
 
+    if (compact) {   // per-row live masks of the compact update field (one ballot per tile row)
+#pragma unroll 1
+      for (int ti = wave; ti < TH; ti += NW) {
+        const uint64_t m = __ballot(lane < TW && kp[ti * TW + (lane < TW ? lane : 0)] != 0);
+        if (lane == 0) a.rmask[(size_t)tile * TH + ti] = m;
+      }
+    }
     PROF_MARK(3);   // compaction
 
     // ---- 32-cell groups ----
@@ -571,7 +582,10 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
 
       // -- epilogue: dx = (dl + tanh(m) * gain) * keep for channels c = (r&3) + 8(r>>2) + 4h --
       if (valid) {
-        float* ob = outb + relcell + (size_t)(4 * h) * HW;
+        // dense: NCHW; compact: [tile][channel][live index]
+        float* ob = compact ? a.out + (size_t)tile * C * NCELL + (size_t)(4 * h) * NCELL + gi
+                            : outb + relcell + (size_t)(4 * h) * HW;
+        const size_t cstr = compact ? (size_t)NCELL : HW;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           float v = accA[r] + accA[r + 8] + accB[r];
@@ -580,7 +594,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
             v = fmaf(fast_tanh(fmaf(bm_, S, accm[r] + accm[r + 8])), (hz && r < 4) ? 0.f : mgain, v);
           }
           if (GNCA_ABLATE & kAblStore) asm volatile("" ::"v"(v));
-          else ob[(size_t)((r & 3) + 8 * (r >> 2)) * HW] = v;
+          else ob[(size_t)((r & 3) + 8 * (r >> 2)) * cstr] = v;
           s1 += v;
           s2 = fmaf(v, v, s2);
         }

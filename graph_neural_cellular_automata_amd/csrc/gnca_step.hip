@@ -149,6 +149,11 @@ struct K1Args {
   const uint8_t* active;   // [B] or null: samples with active[b] == 0 are skipped (K2 copies them)
   const uint8_t* alive;    // [B,H,W] or null: this step's pre-update masks, written by the previous
                            // step's K2 (bit 0: max-pool > alpha_thr, bit 1: > graph_alpha_thr)
+  // compact update field (rollout mode, split K1 only; null = dense NCHW dx in `out`): `out` holds
+  // per tile [C][TH*TW] the live cells' dx in live-cell order; rmask[tile*TH + row] = the row's
+  // live-cell bits, rpre[tile*TH + row] = live cells in the tile's earlier rows
+  uint64_t* rmask;
+  uint32_t* rpre;
   uint64_t seed;
   int64_t rng_step;
   int64_t sample_base;
@@ -1312,6 +1317,10 @@ struct K2Args {
   int use_gn;
   const uint8_t* active;   // [B] or null: inactive samples are copied through unchanged
   int zigzag;              // sample order (below)
+  // compact update field (K1Args::rmask): null = dense dx; else K1's tile geometry
+  const uint64_t* rmask;
+  const uint32_t* rpre;
+  int TH, TW, tiles_x;
 };
 
 // K2's sample for block-row j.  zigzag: K1 sweeps 8 contiguous sample ranges (one per XCD group)
@@ -1352,6 +1361,23 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   float* at = smem;                                  // [(h1-h0) x W] updated alpha
   float* post = smem + (size_t)(a.band + 2) * W;     // [(r1-r0) x W] post-update alive mask
   float* gsh = sh_norm + 4;                          // gamma[C], then beta[C] at +32
+  // compact update field (K1's rollout mode): per (band row incl. halo, K1 tile column) the row's
+  // live mask, live cells before it in its tile, and the tile; per column its (tile column, column
+  // in tile).  dx of a cell = its packed value if live, else 0 (K1 multiplies dead cells by 0).
+  const bool compact = a.rmask != nullptr;
+  const int NCELL = a.TH * a.TW, txn = a.tiles_x;
+  uint64_t* tab_m = reinterpret_cast<uint64_t*>(smem + (size_t)(2 * a.band + 2) * W);
+  uint32_t* tab_p = reinterpret_cast<uint32_t*>(tab_m + (size_t)(a.band + 2) * txn);
+  uint32_t* tab_t = tab_p + (size_t)(a.band + 2) * txn;
+  uint32_t* colinfo = tab_t + (size_t)(a.band + 2) * txn;
+  auto dxc_at = [&](int c, int ii, int j) -> float {
+    const uint32_t ci = colinfo[j];
+    const int e = (ii - h0) * txn + (int)(ci >> 16), tj = (int)(ci & 0xffffu);
+    const uint64_t m = tab_m[e];
+    if (!((m >> tj) & 1ull)) return 0.f;
+    const uint32_t idx = tab_p[e] + (uint32_t)__popcll(m & ((1ull << tj) - 1ull));
+    return a.dx[(size_t)tab_t[e] * C * NCELL + (size_t)c * NCELL + idx];
+  };
 
   // (1) loads: gamma/beta, alpha rows, the first main items (the partials follow below; all in
   //     flight together)
@@ -1366,11 +1392,23 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
     if (e < na) {
       const size_t p = 3 * HW + (size_t)h0 * W + e;
       ax[u] = xb[p];
-      ad[u] = db[p];
+      if (!compact) ad[u] = db[p];
     }
   }
+  if (compact) {
+    const int tr = (h1 - h0) * txn;
+    for (int e = tid; e < tr; e += kThreads) {
+      const int ii = h0 + e / txn, tx = e - (e / txn) * txn;
+      const int ti = ii - (ii / a.TH) * a.TH;
+      const uint32_t t = (uint32_t)((size_t)b * a.tps + (size_t)(ii / a.TH) * txn + tx);
+      tab_m[e] = a.rmask[(size_t)t * a.TH + ti];
+      tab_p[e] = a.rpre[(size_t)t * a.TH + ti];
+      tab_t[e] = t;
+    }
+    for (int j = tid; j < W; j += kThreads) colinfo[j] = ((uint32_t)(j / a.TW) << 16) | (uint32_t)(j % a.TW);
+  }
   vf xv[KU], dv[KU];
-  auto load_items = [&](int it0) {
+  auto load_items = [&](int it0, bool lx, bool ld) {   // dense update field
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       const int it = it0 + u * kThreads;
@@ -1378,13 +1416,13 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
         const int c = it / nv, q = it - c * nv;
         if (c != 3) {
           const size_t p = (size_t)c * HW + base + (size_t)V * q;
-          xv[u] = *reinterpret_cast<const vf*>(xb + p);
-          dv[u] = *reinterpret_cast<const vf*>(db + p);
+          if (lx) xv[u] = *reinterpret_cast<const vf*>(xb + p);
+          if (ld) dv[u] = *reinterpret_cast<const vf*>(db + p);
         }
       }
     }
   };
-  load_items(tid);
+  if (!compact) load_items(tid, true, true);
 
   // (2) per-sample statistics (wave_sum2: fixed order, bit-reproducible)
   if (wave == 0) {
@@ -1415,6 +1453,13 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   __syncthreads();
   const float mu = sh_norm[0], rs = sh_norm[1];
   const float g3 = gn ? gsh[3] : 1.f, b3 = gn ? gsh[32 + 3] : 0.f;
+  if (compact) {   // the tables are in place: the alpha rows' dx and the first main items
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int e = tid + u * kThreads;
+      if (e < na) ad[u] = dxc_at(3, h0 + e / W, e - (e / W) * W);
+    }
+  }
 
   // (3) updated alpha over band + halo, then the post-update alive mask (3x3 max-pool, -inf pad)
   auto alpha_at = [&](float xa, float d) {
@@ -1428,7 +1473,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   }
   for (int e = tid + NA * kThreads; e < na; e += kThreads) {
     const size_t p = 3 * HW + (size_t)h0 * W + e;
-    at[e] = alpha_at(xb[p], db[p]);
+    at[e] = alpha_at(xb[p], compact ? dxc_at(3, h0 + e / W, e - (e / W) * W) : db[p]);
   }
   __syncthreads();
   for (int e = tid; e < nb; e += kThreads) {
@@ -1464,16 +1509,70 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
         for (int k = 0; k < V; ++k) {
           float d = dv[u][k];
           if (gn) d = (d - mu) * gc + bc;
-          v[k] = xv[u][k] + tanhf(d) * a.gain;
+          v[k] = xv[u][k] + fast_tanh(d) * a.gain;
         }
       }
       *reinterpret_cast<vf*>(ob + p) = v;
     }
   };
-  store_items(tid);
-  for (int it0 = tid + KU * kThreads; it0 < nitems; it0 += KU * kThreads) {
-    load_items(it0);
-    store_items(it0);
+  if (!compact) {
+    store_items(tid);
+    for (int it0 = tid + KU * kThreads; it0 < nitems; it0 += KU * kThreads) {
+      load_items(it0, true, true);
+      store_items(it0);
+    }
+  } else {
+    // compact: one thread per cell vector, all channels; the vector's packed-field position and
+    // live ranks are found once (they are the same in every channel plane)
+    for (int q = tid; q < nv; q += kThreads) {
+      const int e = V * q, ii = r0 + e / W, j = e - (e / W) * W;
+      const uint32_t ci = colinfo[j];
+      const int te = (ii - h0) * txn + (int)(ci >> 16), tj = (int)(ci & 0xffffu);
+      const uint64_t m = tab_m[te];
+      const uint32_t bits = (uint32_t)(m >> tj) & ((1u << V) - 1u);
+      const int cnt = __popc(bits);
+      const float* src = a.dx + (size_t)tab_t[te] * C * NCELL + tab_p[te] +
+                         (uint32_t)__popcll(m & ((1ull << tj) - 1ull));
+      int rk[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) rk[k] = ((bits >> k) & 1u) ? __popc(bits & ((1u << k) - 1u)) : -1;
+      const size_t p0 = base + (size_t)e;
+      {   // alpha: x~_3 * post (computed above)
+        vf v;
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = at[(r0 - h0) * W + e + k] * post[e + k];
+        *reinterpret_cast<vf*>(ob + 3 * HW + p0) = v;
+      }
+      constexpr int CU = 5;   // channels in flight per thread (B=1024 72^2: 3 0.164, 5 0.159, 8 0.183 ms)
+      for (int c0 = 0; c0 < C; c0 += CU) {
+        vf xq[CU];
+        float f[CU][V];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+          const int c = c0 + u;
+          if (c >= C || c == 3) continue;
+          xq[u] = *reinterpret_cast<const vf*>(xb + (size_t)c * HW + p0);
+#pragma unroll
+          for (int k = 0; k < V; ++k) f[u][k] = k < cnt ? src[(size_t)c * NCELL + k] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+          const int c = c0 + u;
+          if (c >= C || c == 3) continue;
+          const float gc = gn ? gsh[c] * rs : 1.f, bc = gn ? gsh[32 + c] : 0.f;
+          vf v;
+#pragma unroll
+          for (int k = 0; k < V; ++k) {
+            float d = 0.f;
+#pragma unroll
+            for (int r = 0; r <= k; ++r) d = rk[k] == r ? f[u][r] : d;
+            if (gn) d = (d - mu) * gc + bc;
+            v[k] = xq[u][k] + fast_tanh(d) * a.gain;
+          }
+          *reinterpret_cast<vf*>(ob + (size_t)c * HW + p0) = v;
+        }
+      }
+    }
   }
   if (a.attn) {
     const float amn = sh_norm[2], amx = sh_norm[3];
@@ -1728,8 +1827,11 @@ struct Plan {
   // K2
   int band, nbands, total2;
   size_t lds2;
+  int band_c, nbands_c, total2_c;   // K2 on the compact update field
+  size_t lds2_c;
   // workspace carve (bytes)
-  size_t off_dx, off_stats, off_mm, off_offw, off_alive, ws_bytes;
+  size_t off_dx, off_stats, off_mm, off_offw, off_alive, off_rmask, off_rpre, ws_bytes;
+  bool compact_ok;   // the rollout's compact update field (the 16-channel split K1)
 };
 
 static int max_lds_bytes() { return 160 * 1024; }
@@ -1873,6 +1975,27 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->off_mm = carve((size_t)P->total_tiles * 2 * sizeof(float));
   P->off_offw = carve((size_t)d->B * (P->k > 0 ? P->k : 1) * sizeof(float));
   P->off_alive = carve((size_t)d->B * d->H * d->W);   // rollout: K2 -> next K1 alive bytes
+  // rollout: the compact update field's per-tile-row live masks and prefixes (split K1)
+  // (large batches only: a small batch's K2 needs thin bands to fill the chip, where unpacking the
+  // field costs more than the dx bytes it saves; B=8 72^2: K2 10 -> 18 us)
+  P->compact_ok = P->var->split == 1 && P->var->TH > 0 && !msg_only && !attn_on &&
+                  (long)P->total_tiles >= 2L * device_cus() * (512 / P->var->NT);
+  {
+    // K2 bands on the compact field: ~12 rows (B=1024 72^2: 4 rows 0.233, 8 0.180, 12 0.170,
+    // 24 0.170 ms: the unpacking tables cost a dependent load per workgroup)
+    long rows = 12;
+    static const char* band_env = getenv("GNCA_K2_BAND");   // measurement knob (A/B runs only)
+    if (band_env && atoi(band_env) > 0) rows = atoi(band_env);
+    const long cap = (48L * 1024 / 4 / d->W - 2) / 2;
+    rows = std::max(1L, std::min(rows, cap));
+    P->band_c = (int)rows;
+    P->nbands_c = (d->H + P->band_c - 1) / P->band_c;
+    P->total2_c = P->nbands_c * d->B;
+    P->lds2_c = (size_t)(2 * P->band_c + 2) * d->W * 4 + (size_t)(P->band_c + 2) * P->tiles_x * 16 +
+                (size_t)d->W * 4;
+  }
+  P->off_rmask = carve(P->compact_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint64_t) : 0);
+  P->off_rpre = carve(P->compact_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint32_t) : 0);
   P->ws_bytes = o;
   if (P->need_k0) {
     const size_t k0 = ((size_t)d->C * d->H + d->C + d->d_model + P->k) * sizeof(double);
@@ -2023,7 +2146,7 @@ static bool weights_ok(const gnca_step_desc* d, const gnca_weights* w, bool msg_
 static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float* x, float* x_out,
                      const void* fire, float* attn, void* ws, size_t ws_bytes, hipStream_t st,
                      uint32_t phases = GNCA_PHASE_ALL, const uint8_t* active = nullptr,
-                     bool alive_in = false, bool alive_out = false) {
+                     bool alive_in = false, bool alive_out = false, bool compact = false) {
   Plan P;
   if (!make_plan(d, false, &P)) {
     if (d && d->C >= 4 && d->hidden > 0 && !find_variant(d->C, d->hidden)) return GNCA_ERR_UNSUPPORTED;
@@ -2051,6 +2174,14 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   k1.active = active;
   uint8_t* alive = reinterpret_cast<uint8_t*>(wsb + P.off_alive);
   k1.alive = alive_in ? alive : nullptr;
+  // compact update field (rollout mode): K1 packs the live cells' dx per tile, K2 unpacks them
+  compact = compact && P.compact_ok && !active && !want_attn;
+  uint64_t* rmask = reinterpret_cast<uint64_t*>(wsb + P.off_rmask);
+  uint32_t* rpre = reinterpret_cast<uint32_t*>(wsb + P.off_rpre);
+  if (compact) {
+    k1.rmask = rmask;
+    k1.rpre = rpre;
+  }
   if ((phases & GNCA_PHASE_K1) && (rc = launch_k1(k1, P, st)) != GNCA_OK) return rc;
   if (!(phases & GNCA_PHASE_K2)) return GNCA_OK;
   K2Args k2;
@@ -2062,7 +2193,8 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   k2.attn = (want_attn && P.graph_on) ? attn : nullptr;
   k2.attn_mm = reinterpret_cast<const float*>(wsb + P.off_mm);
   k2.B = d->B; k2.C = d->C; k2.H = d->H; k2.W = d->W; k2.tps = P.tps; k2.nst = P.tps * P.ppt;
-  k2.band = P.band; k2.nbands = P.nbands;
+  k2.band = compact ? P.band_c : P.band;
+  k2.nbands = compact ? P.nbands_c : P.nbands;
   k2.gain = d->update_gain; k2.thr = d->alpha_thr; k2.eps = d->gn_eps;
   k2.gthr = d->graph_alpha_thr;
   k2.alive_out = alive_out ? alive : nullptr;
@@ -2071,7 +2203,15 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   // ms/step (K2 0.182 -> 0.180 ms, the next K1 -0.5 %)
   static const bool zz = getenv("GNCA_K2_ZIGZAG") == nullptr || atoi(getenv("GNCA_K2_ZIGZAG")) != 0;
   k2.zigzag = zz ? 1 : 0;
-  hipLaunchKernelGGL(gnca_k2_finalize, dim3(P.total2), dim3(kThreads), P.lds2, st, k2);
+  if (compact) {
+    k2.rmask = rmask;
+    k2.rpre = rpre;
+    k2.TH = P.TH;
+    k2.TW = P.TW;
+    k2.tiles_x = P.tiles_x;
+  }
+  hipLaunchKernelGGL(gnca_k2_finalize, dim3(compact ? P.total2_c : P.total2), dim3(kThreads),
+                     compact ? P.lds2_c : P.lds2, st, k2);
   return check_launch();
 }
 
@@ -2124,7 +2264,7 @@ int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* 
   else
     snprintf(name, (size_t)n, "gnca_k1_update<%d,%d,%d,%d,%d,%d,%d,%d>", v->CP, v->HDP, v->TH, v->TW, v->RY, v->RX,
              v->KU, v->NT);
-  if (arith) *arith = v->split ? 1 : 0;
+  if (arith) *arith = (v->split ? 1 : 0) | (P.compact_ok ? 2 : 0);
   return GNCA_OK;
 }
 
@@ -2147,7 +2287,7 @@ int gnca_step_phases_f32(const gnca_step_desc* desc, const gnca_weights* w, cons
   const bool alive = (phases & GNCA_PHASE_ALIVE) && desc && desc->alpha_thr >= 0.f &&
                      desc->graph_alpha_thr >= desc->alpha_thr;
   return step_impl(desc, w, x, x_out, fire, attn, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream),
-                   phases, nullptr, alive, alive);
+                   phases, nullptr, alive, alive, (phases & GNCA_PHASE_COMPACT) != 0);
 }
 
 int gnca_message_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
@@ -2238,7 +2378,7 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
     dt.rng_step = desc->rng_step + t;
     if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(dt.offsets, offsets + (size_t)t * 2 * k, 2 * k);
     const int rc = step_impl(&dt, w, src, dst, nullptr, nullptr, ws, ws_bytes, st, GNCA_PHASE_ALL,
-                             nullptr, hand_alive && t > 0, hand_alive && t + 1 < steps);
+                             nullptr, hand_alive && t > 0, hand_alive && t + 1 < steps, true);
     if (rc != GNCA_OK) return rc;
     src = dst;
   }

@@ -124,7 +124,16 @@ def k1_variant(desc: L.StepDesc) -> tuple[str, str]:
     buf = ctypes.create_string_buffer(128)
     arith = ctypes.c_int32(0)
     L.check(L.load().gnca_k1_variant(ctypes.byref(desc), buf, 128, ctypes.byref(arith)), "gnca_k1_variant")
-    return buf.value.decode(), ("bf16x6" if arith.value == 1 else "f32")
+    return buf.value.decode(), ("bf16x6" if arith.value & 1 else "f32")
+
+
+def rollout_compact(desc: L.StepDesc) -> bool:
+    """True when a rollout of ``desc``'s shape runs on the compact update field (K1 packs the live
+    cells' dx per tile, K2 unpacks them: GNCA_PHASE_COMPACT)."""
+    buf = ctypes.create_string_buffer(128)
+    arith = ctypes.c_int32(0)
+    L.check(L.load().gnca_k1_variant(ctypes.byref(desc), buf, 128, ctypes.byref(arith)), "gnca_k1_variant")
+    return bool(arith.value & 2)
 
 
 def stream_ptr(device) -> int:

@@ -118,7 +118,8 @@ size_t gnca_workspace_bytes(const gnca_step_desc* desc);
 /* Measurement: the K1 kernel the plan for `desc` launches, as "name<template args>" (NUL-terminated,
  * truncated to n bytes), and its MFMA arithmetic in *arith (may be NULL): 0 = fp32 MFMA
  * (v_mfma_f32_*_f32), 1 = bf16 MFMA on exact 3-way splits of the fp32 operands (6 products per
- * fp32 product, gnca_k1_split.h).  Host-only.  Returns GNCA_OK or GNCA_ERR_INVALID. */
+ * fp32 product, gnca_k1_split.h), plus 2 when a rollout of this shape uses the compact update field
+ * (GNCA_PHASE_COMPACT).  Host-only.  Returns GNCA_OK or GNCA_ERR_INVALID. */
 int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* arith);
 
 /*
@@ -154,6 +155,11 @@ int gnca_step_masked_f32(const gnca_step_desc* desc, const gnca_weights* w, cons
  * and K1 reads them (what gnca_rollout_f32 does for every step after the first; needs
  * 0 <= alpha_thr <= graph_alpha_thr, and a K2 call with this bit on the same workspace first). */
 #define GNCA_PHASE_ALIVE (1u << 3)
+/* Rollout mode's compact update field (what gnca_rollout_f32 does for every step when the planned
+ * K1 is the 16-channel split kernel): K1 writes dx only for its live cells, packed per tile in
+ * live-cell order with per-tile-row live masks, and K2 reads them back (dead cells have dx = 0).
+ * Both the K1 and the K2 call of a step must carry it; ignored for other K1 variants. */
+#define GNCA_PHASE_COMPACT (1u << 4)
 int gnca_step_phases_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
                          float* x_out, const void* fire, float* attn, void* ws, size_t ws_bytes,
                          void* stream, uint32_t phases);

@@ -1,5 +1,6 @@
 """GPU tests of the nn.Module surface: the reference's call pattern, RNG contract on device,
 property checks at the benchmark's full size (B=1024 x 16 x 72 x 72)."""
+import ctypes
 import random
 
 import numpy as np
@@ -165,6 +166,55 @@ def test_full_size_determinism_and_shard_invariance(dev):
     one, _ = S.step(d, w, xs)
     ref = O.nca_step(xs.cpu().numpy().astype(np.float64), p, cfg, chosen=offs[0], fire_mask=fm)
     np.testing.assert_allclose(one.cpu().numpy(), ref, rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_compact_rollout_equals_dense_steps(dev, graph):
+    """The rollout's compact update field (K1 packs the live cells' dx per tile with per-row live
+    masks, K2 unpacks them; GNCA_PHASE_COMPACT) gives bitwise the states of repeated single steps
+    on the dense NCHW field, at a batch that plans the large-batch split K1 (24x36 tiles) and in
+    the classic step; and the phase API in compact mode equals the rollout."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    m = _trained_like(dev, seed=6)
+    B, steps = 128, 3
+    x = _state(B, 16, 72, 72, dev, seed=21)
+    random.seed(13)
+    offs = [random.sample(m.graph.offsets, 8) if graph else [] for _ in range(steps)]
+    tensors = dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
+                   b1=m.update_net[0].bias, w2=m.update_net[2].weight, gn_weight=m.norm.weight,
+                   gn_bias=m.norm.bias)
+    if graph:
+        tensors.update(m.graph.weight_tensors())
+    w, keep = S.make_weights(tensors)
+    flags = L.USE_GROUPNORM | ((L.GRAPH | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE) if graph else 0)
+
+    def desc(t):
+        return S.make_desc(B=B, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[t], flags=flags,
+                           update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                           fire_mode=L.FIRE_HASH, rng_seed=42, rng_step=t)
+
+    name, arith = S.k1_variant(desc(0))
+    assert arith == "bf16x6", name
+    r = S.rollout(desc(0), w, x.contiguous(), steps, offs)
+    cur = x
+    for t in range(steps):
+        cur, _ = S.step(desc(t), w, cur)
+    assert torch.equal(r, cur)
+    # the phase API in rollout mode (K1 and K2 calls with PHASE_COMPACT [| PHASE_ALIVE])
+    lib = L.load()
+    ws = S.workspace(desc(0), dev)
+    src, bufs = x.contiguous(), [torch.empty_like(x), torch.empty_like(x)]
+    st = torch.cuda.current_stream().cuda_stream
+    for t in range(steps):
+        d, dst = desc(t), bufs[t % 2]
+        for ph in (L.PHASE_K1 | L.PHASE_COMPACT | (L.PHASE_ALIVE if t > 0 else 0),
+                   L.PHASE_K2 | L.PHASE_COMPACT | L.PHASE_ALIVE):
+            L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), src.data_ptr(),
+                                             dst.data_ptr(), None, None, ws.data_ptr(), ws.numel(),
+                                             st, ph), "phases")
+        src = dst
+    assert torch.equal(src, r)
 
 
 def test_long_rollout_drift(dev):

@@ -76,11 +76,11 @@ def run(reps=15, rounds=3):
     ws = torch.empty(next(iter(libs.values())).gnca_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream()
     # rollout mode (default): K1 reads the alive bytes a primed K2 wrote (GNCA_PHASE_ALIVE)
-    ph = int(os.environ.get("ABLATE_PHASES", str(L.PHASE_K1 | L.PHASE_ALIVE)))
+    ph = int(os.environ.get("ABLATE_PHASES", str(L.PHASE_K1 | L.PHASE_ALIVE | L.PHASE_COMPACT)))
     if ph & L.PHASE_ALIVE:
         assert next(iter(libs.values())).gnca_step_phases_f32(
             ctypes.byref(d), ctypes.byref(w), x.data_ptr(), out.data_ptr(), None, None, ws.data_ptr(),
-            ws.numel(), st.cuda_stream, L.PHASE_ALL | L.PHASE_ALIVE) == 0
+            ws.numel(), st.cuda_stream, L.PHASE_ALL | L.PHASE_ALIVE | L.PHASE_COMPACT) == 0
     res = {n: [] for n in libs}
     for _ in range(rounds):
         for n, lib in libs.items():
