@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_gnprep(const BAArgs a) {
     const float g3 = gn ? a.gamma[3] : 1.f, b3 = gn ? a.beta[3] : 0.f;
     auto alpha_at = [&](float xa, float d) {
       if (gn) d = (d - mu) * rs * g3 + b3;   // the forward K2's expression for alpha
-      return xa + tanhf(d) * a.gain;
+      return xa + fast_tanh(d) * a.gain;   // K2's expression, bit for bit
     };
 #pragma unroll
     for (int u = 0; u < NA; ++u) {

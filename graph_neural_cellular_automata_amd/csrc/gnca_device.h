@@ -45,6 +45,13 @@ __device__ __forceinline__ bool fire_at(int mode, const void* fire, float rate, 
   return true;
 }
 
+// tanh(x) = 1 - 2 / (exp(2x) + 1): v_exp + v_rcp; abs error ~2e-7 (saturates to +-1, NaN-preserving).
+// K2's update tanh (and BA's recompute of the updated alpha, which must give K2's gate bits).
+__device__ __forceinline__ float fast_tanh(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // exp(2x)
+  return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+}
+
 __host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
 __host__ __device__ constexpr int odd4(int v) {  // round up to 4*odd: conflict-free 16-lane b128
   return ((((v + 3) & ~3) >> 2) & 1) ? ((v + 3) & ~3) : ((v + 3) & ~3) + 4;

@@ -169,11 +169,6 @@ struct K1Args {
 // hipcc does not insert the MFMA-result read hazard wait states around an asm statement.
 __device__ __forceinline__ float relu_nan(float v) { return __builtin_elementwise_maximum(v, 0.f); }
 
-// tanh(x) = 1 - 2 / (exp(2x) + 1): v_exp + v_rcp; abs error ~2e-7 (saturates to +-1, NaN-preserving)
-__device__ __forceinline__ float fast_tanh(float x) {
-  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // exp(2x)
-  return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
-}
 
 }  // namespace gnca
 
@@ -1464,7 +1459,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   // (3) updated alpha over band + halo, then the post-update alive mask (3x3 max-pool, -inf pad)
   auto alpha_at = [&](float xa, float d) {
     if (gn) d = (d - mu) * rs * g3 + b3;
-    return xa + tanhf(d) * a.gain;
+    return xa + fast_tanh(d) * a.gain;   // as the backward's BA (the same gate bits)
   };
 #pragma unroll
   for (int u = 0; u < NA; ++u) {
