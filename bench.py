@@ -58,7 +58,7 @@ WORKLOADS = {
 }
 # per-launch HBM traffic of K1/K2 measured by rocprofv3 PMC counters in separate passes
 # (tools/pmc.sh + tools/pmc_traffic.py); counters cannot be read from inside this process
-PMC_TRAFFIC = max(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic.json")) or
+PMC_TRAFFIC = max(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc_traffic.json")) or
                   [os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")])
 
 
