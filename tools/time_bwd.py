@@ -1,6 +1,6 @@
 """Time the step forward and backward (C ABI) at a few sizes; prints one line per size.
 
-usage: python tools/time_bwd.py [--sizes 1024x72,16x40] [--iters 20]
+usage: python tools/time_bwd.py [--sizes 1024x72,16x40] [--iters 20] [--channels 32 --radius 5 --k 16]
 """
 from __future__ import annotations
 
@@ -23,10 +23,15 @@ def main():
     ap.add_argument("--sizes", default="1024x72,16x40")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--zp", action="store_true")
+    ap.add_argument("--channels", type=int, default=16)
+    ap.add_argument("--radius", type=int, default=4)
+    ap.add_argument("--k", type=int, default=8)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    model = NeuralCAGraph(16, 128, update_gain=0.05, alpha_thr=0.12, message_gain=0.25,
+    C = args.channels
+    model = NeuralCAGraph(C, 128, update_gain=0.05, alpha_thr=0.12, message_gain=0.25,
+                          graph_attention_radius=args.radius, graph_num_neighbors=args.k,
                           graph_zero_padded_shift=args.zp).to(dev)
     with torch.no_grad():
         model.update_net[2].weight.normal_(0, 0.05)
@@ -37,14 +42,14 @@ def main():
     w, keep = S.make_weights(tensors)
     want = {n: p for n, p in model.named_parameters() if n in S.GRAD_FIELDS}
     random.seed(1)
-    chosen = random.sample(model.graph.offsets, 8)
+    chosen = random.sample(model.graph.offsets, args.k)
     flags = L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE | (L.ZERO_PAD_SHIFT if args.zp else 0)
     for spec in args.sizes.split(","):
         B, S_ = (int(v) for v in spec.split("x"))
-        x = torch.rand(B, 16, S_, S_, device=dev)
-        x[:, 4:] = torch.randn(B, 12, S_, S_, device=dev)
+        x = torch.rand(B, C, S_, S_, device=dev)
+        x[:, 4:] = torch.randn(B, C - 4, S_, S_, device=dev)
         gy = torch.randn_like(x)
-        d = S.make_desc(B=B, C=16, H=S_, W=S_, hidden=128, d_model=16, offsets=chosen, flags=flags,
+        d = S.make_desc(B=B, C=C, H=S_, W=S_, hidden=128, d_model=16, offsets=chosen, flags=flags,
                         update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
                         fire_mode=L.FIRE_HASH, rng_seed=3)
         for _ in range(3):
@@ -69,7 +74,7 @@ def main():
         b = e1.elapsed_time(e2) / args.iters
         bs = e2.elapsed_time(e3) / args.iters
         cells = B * S_ * S_
-        print(f"B={B} {S_}x{S_} zp={int(args.zp)}: fwd {f:.3f} ms  bwd(recompute) {b:.3f} ms  "
+        print(f"B={B} C={C} {S_}x{S_} zp={int(args.zp)}: fwd {f:.3f} ms  bwd(recompute) {b:.3f} ms  "
               f"bwd(saved) {bs:.3f} ms  bwd/fwd {bs / f:.2f}  "
               f"fwd+bwd {cells / ((f + bs) * 1e-3) / 1e9:.3f} G cell/s", flush=True)
 
