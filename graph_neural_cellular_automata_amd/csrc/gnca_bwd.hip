@@ -1537,7 +1537,13 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
         const size_t bytes = (size_t)L.total * 4;
         if (bytes > 160 * 1024) continue;
         const long tx = (W + tw - 1) / tw, ty = (H + th - 1) / th;
-        const double tcost = (double)tx * ty * th * tw + 0.01 * tx * ty * L.RH * L.RW * P->CP + 30.0 * tx * ty;
+        // makespan of the persistent grid (min(CUs, tiles) workgroups): rounds x per-tile cost, so
+        // a batch that cannot fill the chip takes the tile that finishes in the fewest rounds
+        // (B=16 40^2: 8x8 tiles = 400 tiles = 2 rounds on 256 CUs)
+        const long tiles = (long)d->B * tx * ty, cus = bwd_device_cus();
+        const long rounds = (tiles + cus - 1) / cus;
+        const double per_tile = (double)th * tw + 0.01 * L.RH * L.RW * P->CP + 30.0;
+        const double tcost = (double)std::max<long>(rounds * cus, tiles) * per_tile;
         const double cost = 1e12 * ns + 1e9 * padh + tcost;
         if (cost < best) {
           best = cost; P->bb = &v; P->TH = th; P->TW = tw; P->ldsB = bytes;
@@ -1552,9 +1558,11 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   P->total_tiles = P->tps * d->B;
   P->gridB = std::min(bwd_device_cus(), P->total_tiles);
   if (P->gridB < 1) P->gridB = 1;
-  // BA bands (as the forward K2)
+  // BA bands: ~8 per sample, thinner when the batch cannot give every CU two workgroups
+  // (B=16 128^2 32ch: 16-row bands = 128 workgroups on 256 CUs)
   {
-    long rows = (H + 7) / 8;
+    const long nb_target = std::max<long>(8, (2L * bwd_device_cus() + d->B - 1) / d->B);
+    long rows = (H + nb_target - 1) / nb_target;
     const long cap = (48L * 1024 / 4 / W - 2) / 2;
     if (rows > cap) rows = cap;
     if (rows < 1) rows = 1;

@@ -77,6 +77,8 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   const int h = lane >> 5, r32 = lane & 31;
   const int H = a.H, W = a.W;
   const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
+  const bool compact = a.rmask != nullptr;   // the rollout's compact update field (gnca_k1_split.h)
+  static_assert(TW <= 64, "one ballot per tile row (compact update field)");
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
 
@@ -292,15 +294,23 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
         off += w_ < wave ? wcnt[w_] : 0;
         nlive += wcnt[w_];
       }
+      if (compact && inb && n % TW == 0) a.rpre[(size_t)tile * TH + n / TW] = (uint32_t)(off + pre);
       if (live) {
         lst[off + pre] = (uint16_t)n;
-      } else if (inb) {
+      } else if (inb && !compact) {
         const int ti = n / TW, tj = n - (n / TW) * TW;
         float* oz = outb + (size_t)ti * W + tj;
 #pragma unroll
         for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
       }
       __syncthreads();
+    }
+    if (compact) {   // per-row live masks of the compact update field
+#pragma unroll 1
+      for (int ti_ = wave; ti_ < TH; ti_ += NW) {
+        const uint64_t m = __ballot(lane < TW && kp[ti_ * TW + (lane < TW ? lane : 0)] != 0);
+        if (lane == 0) a.rmask[(size_t)tile * TH + ti_] = m;
+      }
     }
 
     // ---- one 32-cell group per wave; its accumulators live across the two channel phases ----
@@ -482,13 +492,16 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
 
       // -- epilogue: dx = (dl + tanh(m) * gain) * keep for channels c = (r&3) + 8(r>>2) + 4h --
       if (valid) {
-        float* ob = outb + (size_t)(ti * W + tj) + (size_t)(4 * h) * HW;
+        // dense: NCHW; compact: [tile][channel][live index]
+        float* ob = compact ? a.out + (size_t)tile * C * NCELL + (size_t)(4 * h) * NCELL + gi
+                            : outb + (size_t)(ti * W + tj) + (size_t)(4 * h) * HW;
+        const size_t cstr = compact ? (size_t)NCELL : HW;
         const float* bmp = reinterpret_cast<const float*>(smem_b + L.bml) + 16 * h;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float v = accD[r];
           if constexpr (GRAPH) v = fmaf(fast_tanh(fmaf(bmp[r], S, accm[r])), (hz && r < 4) ? 0.f : mgain, v);
-          ob[(size_t)((r & 3) + 8 * (r >> 2)) * HW] = v;
+          ob[(size_t)((r & 3) + 8 * (r >> 2)) * cstr] = v;
           s1 += v;
           s2 = fmaf(v, v, s2);
         }

@@ -1334,7 +1334,7 @@ __device__ __forceinline__ int k2_sample(int j, int B, int zigzag) {
 // the band needs first (GroupNorm partials, alpha rows, gamma/beta and the first KU main items)
 // is issued before the first barrier: a small-batch launch waits out one memory latency, not
 // one per phase.
-template <int V>
+template <int V, bool COMPACT>
 __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_norm) {
   typedef float vf __attribute__((ext_vector_type(V)));
   constexpr int KU = 2;   // main items per thread in flight (measured: 1: 0.184, 2: 0.178, 4: 0.187, 8: 0.207 ms)
@@ -1359,7 +1359,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   // compact update field (K1's rollout mode): per (band row incl. halo, K1 tile column) the row's
   // live mask, live cells before it in its tile, and the tile; per column its (tile column, column
   // in tile).  dx of a cell = its packed value if live, else 0 (K1 multiplies dead cells by 0).
-  const bool compact = a.rmask != nullptr;
+  constexpr bool compact = COMPACT;
   const int NCELL = a.TH * a.TW, txn = a.tiles_x;
   uint64_t* tab_m = reinterpret_cast<uint64_t*>(smem + (size_t)(2 * a.band + 2) * W);
   uint32_t* tab_p = reinterpret_cast<uint32_t*>(tab_m + (size_t)(a.band + 2) * txn);
@@ -1578,6 +1578,9 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   }
 }
 
+// one instantiation per (cell-vector width, update-field layout): each gets its own registers
+// (compact, B=1024: 75 VGPRs, 6 waves/SIMD; capping it at 64 for 8 waves measured 0.178 vs 0.163 ms)
+template <int V, bool COMPACT>
 __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float sh_norm[4 + 64];
@@ -1596,8 +1599,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
     }
     return;
   }
-  if ((a.W & 3) == 0) k2_body<4>(a, smem, sh_norm);
-  else k2_body<1>(a, smem, sh_norm);
+  k2_body<V, COMPACT>(a, smem, sh_norm);
 }
 
 // normalise a message-only attention map (no K2 in message mode)
@@ -1826,7 +1828,7 @@ struct Plan {
   size_t lds2_c;
   // workspace carve (bytes)
   size_t off_dx, off_stats, off_mm, off_offw, off_alive, off_rmask, off_rpre, ws_bytes;
-  bool compact_ok;   // the rollout's compact update field (the 16-channel split K1)
+  bool compact_ok;   // the rollout's compact update field (the bf16-split K1s, large batches)
 };
 
 static int max_lds_bytes() { return 160 * 1024; }
@@ -1973,7 +1975,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // rollout: the compact update field's per-tile-row live masks and prefixes (split K1)
   // (large batches only: a small batch's K2 needs thin bands to fill the chip, where unpacking the
   // field costs more than the dx bytes it saves; B=8 72^2: K2 10 -> 18 us)
-  P->compact_ok = P->var->split == 1 && P->var->TH > 0 && !msg_only && !attn_on &&
+  P->compact_ok = P->var->split > 0 && P->var->TH > 0 && !msg_only && !attn_on &&
                   (long)P->total_tiles >= 2L * device_cus() * (512 / P->var->NT);
   {
     // K2 bands on the compact field: ~12 rows (B=1024 72^2: 4 rows 0.233, 8 0.180, 12 0.170,
@@ -2205,7 +2207,9 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
     k2.TW = P.TW;
     k2.tiles_x = P.tiles_x;
   }
-  hipLaunchKernelGGL(gnca_k2_finalize, dim3(compact ? P.total2_c : P.total2), dim3(kThreads),
+  auto k2fn = compact ? ((d->W & 3) == 0 ? gnca_k2_finalize<4, true> : gnca_k2_finalize<1, true>)
+                      : ((d->W & 3) == 0 ? gnca_k2_finalize<4, false> : gnca_k2_finalize<1, false>);
+  hipLaunchKernelGGL(k2fn, dim3(compact ? P.total2_c : P.total2), dim3(kThreads),
                      compact ? P.lds2_c : P.lds2, st, k2);
   return check_launch();
 }

@@ -145,13 +145,13 @@ def test_k1_variant_names(lib):
     assert name(8, 16, 72, r4) == ("gnca_k1_split<8,24,4,4,8>", "bf16x6")
     assert name(8, 16, 72, [], graph=False) == ("gnca_k1_split<8,24,1,4,0>", "bf16x6")
     assert name(128, 32, 128, r5) == ("gnca_k1_split32<16,16,5,5,16>", "bf16x6")
-    # the rollout's compact update field: large batches on the 16-channel split K1 only
+    # the rollout's compact update field: large batches on the bf16-split K1s only
     comp = lambda B, C, H, offs, graph=True: S.rollout_compact(S.make_desc(
         B=B, C=C, H=H, W=H, hidden=128, d_model=16, offsets=offs,
         flags=flags if graph else L_.USE_GROUPNORM, update_gain=0.05, alpha_thr=0.12,
         message_gain=0.25, fire_rate=0.5, fire_mode=L_.FIRE_HASH))
     assert comp(1024, 16, 72, r4) and comp(1024, 16, 72, [], graph=False)
-    assert not comp(8, 16, 72, r4) and not comp(128, 32, 128, r5)
+    assert not comp(8, 16, 72, r4) and comp(128, 32, 128, r5) and not comp(4, 32, 128, r5)
     nm, ar = name(4, 12, 20, r4, hidden=64)
     assert nm.startswith("gnca_k1_update<12,64,") and ar == "f32"
     buf = ctypes.create_string_buffer(8)
