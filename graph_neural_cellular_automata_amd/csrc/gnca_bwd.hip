@@ -1774,8 +1774,12 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     a.active = active;
     a.B = B; a.C = C; a.H = H; a.W = W; a.k = P.msg ? P.F.k : 0;
     a.TH = P.TH3; a.TW = P.TW3; a.tiles_x = P.tiles_x3; a.tps = P.tps3;
-    // channel groups: enough workgroups to fill the chip when the batch is small
-    const long wgs = (long)B * P.tps3, want = 2L * bwd_device_cus();
+    // channel groups: enough workgroups to fill the chip when the batch is small, ~4 per CU (each
+    // walks its channels one memory round trip at a time; B=16 128^2 32ch bwd: 2 per CU 1.456,
+    // 4 1.382, 8 1.392, 16 1.411 ms; tools/bc_sweep.sh)
+    static const char* ncg_env = getenv("GNCA_BC_WGS_PER_CU");   // measurement knob (A/B runs only)
+    const long per_cu = ncg_env && atoi(ncg_env) > 0 ? atoi(ncg_env) : 4;
+    const long wgs = (long)B * P.tps3, want = per_cu * bwd_device_cus();
     a.ncg = (int)std::min<long>(C, std::max<long>(1, (want + wgs - 1) / wgs));
     a.cpw = (C + a.ncg - 1) / a.ncg;
     a.ncg = (C + a.cpw - 1) / a.cpw;
