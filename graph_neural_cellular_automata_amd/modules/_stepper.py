@@ -140,12 +140,63 @@ def apply_step(model: nn.Module, x, desc, weights, keep, fire, want_attn=False, 
     return _StepFn.apply(x, desc, weights, keep, fire, want_attn, active, core, graph, tc, tg, tensors)
 
 
+def _step_tensors(model: nn.Module, graph) -> dict:
+    """The step's weight tensors by short name, read straight from the modules' parameter dicts
+    (``nn.Module.__getattr__`` costs ~1 us per attribute: building this dict through it was ~30 us
+    of host time per step at the trainer's size, more than the step's kernels)."""
+    mods = model._modules
+    up = mods["update_net"]._modules
+    l1, l2 = up["0"]._parameters, up["2"]._parameters
+    t = {"perception": mods["perception"]._modules["conv"]._parameters["weight"],
+         "w1": l1["weight"], "b1": l1["bias"], "w2": l2["weight"]}
+    norm = mods["norm"]
+    if isinstance(norm, nn.GroupNorm):
+        t["gn_weight"] = norm._parameters["weight"]
+        t["gn_bias"] = norm._parameters["bias"]
+    if graph is not None:
+        gm = graph._modules
+        q, k, m = (gm[n]._parameters for n in ("query_proj", "key_proj", "msg_proj"))
+        t.update(wq=q["weight"], bq=q["bias"], wk=k["weight"], bk=k["bias"], wm=m["weight"], bm=m["bias"],
+                 scaling=graph._parameters["scaling"])
+    return t
+
+
+_DESC_TEMPLATES: dict = {}
+
+
+def _step_desc(key, chosen, message_gain, fire_rate, fire_mode):
+    """A fresh descriptor: the fields fixed by (shape, flags, model constants) copied from a cached
+    template, then this call's offsets, message gain and fire fields (make_desc was ~10 us)."""
+    tpl = _DESC_TEMPLATES.get(key)
+    if tpl is None:
+        B, C, H, W, hidden, d_model, flags, update_gain, alpha_thr, graph_thr, eps = key
+        tpl = S.make_desc(B=B, C=C, H=H, W=W, hidden=hidden, d_model=d_model, offsets=[], flags=flags,
+                          update_gain=update_gain, alpha_thr=alpha_thr, graph_alpha_thr=graph_thr,
+                          message_gain=0.0, fire_rate=1.0, fire_mode=L.FIRE_NONE, gn_eps=eps)
+        if len(_DESC_TEMPLATES) >= 256:
+            _DESC_TEMPLATES.clear()
+        _DESC_TEMPLATES[key] = tpl
+    d = L.StepDesc.from_buffer_copy(tpl)
+    if chosen:
+        if len(chosen) > L.MAX_OFFSETS:
+            raise ValueError(f"at most {L.MAX_OFFSETS} offsets per step (got {len(chosen)})")
+        flat = [v for o in chosen for v in o]
+        if min(flat) < -127 or max(flat) > 127:
+            raise ValueError(f"offsets {chosen} out of int8 range")
+        d.num_offsets = len(chosen)
+        d.offsets[:len(flat)] = flat
+    d.message_gain = float(message_gain)
+    d.fire_rate = float(fire_rate)
+    d.fire_mode = fire_mode
+    return d
+
+
 def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen, message_gain,
              hidden_only: bool, return_attention: bool, active=None):
     x = S.check_state(x, model.n_channels)
     B, C, H, W = x.shape
     flags = 0
-    norm = model.norm
+    norm = model._modules["norm"]
     eps = 1e-3
     if isinstance(norm, nn.GroupNorm):
         if norm.num_groups != 1 or not norm.affine:
@@ -154,17 +205,13 @@ def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen,
         eps = norm.eps
     elif not isinstance(norm, nn.Identity):
         raise ValueError(f"unsupported norm module {type(norm).__name__}")
-    tensors = dict(perception=model.perception.conv.weight, w1=model.update_net[0].weight,
-                   b1=model.update_net[0].bias, w2=model.update_net[2].weight)
-    if flags & L.USE_GROUPNORM:
-        tensors.update(gn_weight=norm.weight, gn_bias=norm.bias)
+    tensors = _step_tensors(model, graph)
     d_model = 1
     graph_thr = None
     if graph is not None:
         flags |= graph.flags(return_attention)
         if hidden_only:
             flags |= L.HIDDEN_ONLY
-        tensors.update(graph.weight_tensors())
         d_model = graph.d_model
         graph_thr = graph.alpha_thr
     # stochastic fire mask: the reference's torch.rand draw, on x.device (ncagraph.py:144-146)
@@ -173,11 +220,10 @@ def run_step(model: nn.Module, x: torch.Tensor, fire_rate: float, graph, chosen,
     if fire_rate < 1.0:
         fire = torch.rand(B, 1, H, W, device=x.device)
         fire_mode = L.FIRE_RAND_F32
-    desc = S.make_desc(B=B, C=C, H=H, W=W, hidden=model.update_net[0].out_channels,
-                       d_model=d_model, offsets=chosen or [], flags=flags,
-                       update_gain=model.update_gain, alpha_thr=model.alpha_thr,
-                       graph_alpha_thr=graph_thr, message_gain=message_gain,
-                       fire_rate=fire_rate, fire_mode=fire_mode, gn_eps=eps)
+    alpha_thr = float(model.alpha_thr)
+    key = (B, C, H, W, tensors["w1"].shape[0], d_model, flags, float(model.update_gain), alpha_thr,
+           alpha_thr if graph_thr is None else float(graph_thr), float(eps))
+    desc = _step_desc(key, chosen, message_gain, fire_rate, fire_mode)
     w, keep = S.make_weights(tensors)
     if torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in tensors.values())):
         out, attn = apply_step(model, x, desc, w, keep, fire, return_attention, active, tensors)

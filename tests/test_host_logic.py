@@ -105,3 +105,54 @@ def test_helpers_match_reference_semantics():
     pol = m._apply_message_policy(x)
     assert (pol[:, :4] == 0).all()
     torch.testing.assert_close(pol[:, 4:], torch.tanh(x[:, 4:]) * 0.7)
+
+
+def test_run_step_fast_host_path_matches_reference_accessors():
+    """The module step's host fast path (_step_tensors: parameter dicts instead of
+    nn.Module.__getattr__; _step_desc: cached descriptor templates) builds exactly the weight set
+    and the descriptor bytes of the plain path (attribute access + make_desc), for the graph and
+    classic modules, with and without GroupNorm, including after the caller changes alpha_thr,
+    message_gain and the offsets between calls."""
+    import ctypes
+    import random
+
+    import torch.nn as nn
+
+    from graph_neural_cellular_automata_amd import NeuralCA, NeuralCAGraph
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    from graph_neural_cellular_automata_amd.modules._stepper import _step_desc, _step_tensors
+
+    for model, graph in ((NeuralCAGraph(16, 64, update_gain=0.05, alpha_thr=0.12), True),
+                         (NeuralCAGraph(8, 32, use_groupnorm=False, graph_zero_padded_shift=False), True),
+                         (NeuralCA(12, 48, update_gain=0.1, alpha_thr=0.1), False)):
+        g = model.graph if graph else None
+        want = dict(perception=model.perception.conv.weight, w1=model.update_net[0].weight,
+                    b1=model.update_net[0].bias, w2=model.update_net[2].weight)
+        if isinstance(model.norm, nn.GroupNorm):
+            want.update(gn_weight=model.norm.weight, gn_bias=model.norm.bias)
+        if graph:
+            want.update(g.weight_tensors())
+        got = _step_tensors(model, g)
+        assert set(got) == set(want) and all(got[k] is want[k] for k in want)
+        random.seed(3)
+        for trial in range(3):
+            model.alpha_thr = 0.1 + 0.05 * trial
+            chosen = g.sample_offsets() if graph else []
+            flags = (g.flags(False) | L.HIDDEN_ONLY) if graph else 0
+            if isinstance(model.norm, nn.GroupNorm):
+                flags |= L.USE_GROUPNORM
+            mg, fr = 0.25 * trial, (1.0 if trial == 0 else 0.6)
+            fm = L.FIRE_NONE if fr >= 1.0 else L.FIRE_RAND_F32
+            C = model.n_channels
+            ref = S.make_desc(B=3, C=C, H=20, W=24, hidden=model.update_net[0].out_channels,
+                              d_model=g.d_model if graph else 1, offsets=chosen, flags=flags,
+                              update_gain=model.update_gain, alpha_thr=model.alpha_thr,
+                              graph_alpha_thr=g.alpha_thr if graph else None, message_gain=mg,
+                              fire_rate=fr, fire_mode=fm, gn_eps=1e-3)
+            key = (3, C, 20, 24, model.update_net[0].out_channels, g.d_model if graph else 1, flags,
+                   float(model.update_gain), float(model.alpha_thr),
+                   float(g.alpha_thr) if graph else float(model.alpha_thr), 1e-3)
+            d = _step_desc(key, chosen, mg, fr, fm)
+            assert ctypes.string_at(ctypes.addressof(d), ctypes.sizeof(d)) == \
+                ctypes.string_at(ctypes.addressof(ref), ctypes.sizeof(ref))
