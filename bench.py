@@ -245,13 +245,28 @@ def main_train(args, dev, world, rank):
     # (offset draws, fire rates, short/long regime) stays in lockstep on every rank
     stab_rng = random.Random(4242 + rank)
     cells = [0]
+    # GNCA_TRAIN_PHASES=1 (measurement only): synchronise at the phase boundaries and report the
+    # mean wall time of each phase of an iteration on stderr
+    phase_t = {} if os.environ.get("GNCA_TRAIN_PHASES") else None
 
-    def iteration():
+    def mark(name, t_prev):
+        if phase_t is None:
+            return t_prev
+        torch.cuda.synchronize()
+        t_now = time.perf_counter()
+        phase_t[name] = phase_t.get(name, 0.0) + t_now - t_prev
+        return t_now
+
+    def iteration(warm_alloc=False):
+        tp = mark("sync", time.perf_counter()) if phase_t is not None else None
         idx, state = pool.sample(B)
         if twl["damage"]:
             apply_damage_policy_(state, DAMAGE_CFG, epoch=DAMAGE_CFG["start_epoch"])
             stats["damage_calls"] += 1
         lo, hi = long_ if random.random() < long_prob else short
+        if warm_alloc:   # untimed warmup: the longest rollout once, so the timed iterations run on a
+            lo = hi = long_[1]   # grown caching allocator (a trainer's steady state after its first
+                                 # long rollout) instead of paying hipMalloc for new activation blocks
         stats["long_rollouts"] += int(lo == long_[0])
         nsteps = torch.randint(lo, hi + 1, (B,), device=dev, generator=gen)
         T = int(nsteps.max().item())
@@ -260,6 +275,7 @@ def main_train(args, dev, world, rank):
             model.message_gain = MSG_GAIN if t % 3 == 0 else 0.0   # message_every = 3
             state = model(state, fire_rate=fr, active=nsteps > t)
         model.message_gain = MSG_GAIN
+        tp = mark("sample+rollout", tp)
         cells[0] += int(nsteps.sum().item()) * H * H
         per_sample = loss_premult_rgba(state[:, :4], target[None])   # fused HIP loss (fwd+bwd)
         loss = per_sample.mean()
@@ -279,16 +295,19 @@ def main_train(args, dev, world, rank):
                     loss = loss + 0.5 * F.mse_loss(st[close, :4], target[None].expand(B, -1, -1, -1)[close])
                 stats["stability_samples"] += n
                 cells[0] += 24 * n * H * H
+        tp = mark("loss+stability", tp)
         opt.zero_grad(set_to_none=True)
         loss.backward()
+        tp = mark("backward", tp)
         allreduce_gradients(params)
         normalize_gradients_(params)
         opt.step()
         pool.replace(idx, state.detach())
+        mark("allreduce+adam+pool", tp)
         return loss
 
-    for _ in range(args.warmup):
-        iteration()
+    for w_ in range(args.warmup):
+        iteration(warm_alloc=w_ == 0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -297,12 +316,17 @@ def main_train(args, dev, world, rank):
     for k_ in stats:
         stats[k_] = 0
     t0 = time.perf_counter()
+    if phase_t is not None:
+        phase_t.clear()
     for _ in range(args.steps):
         loss = iteration()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    if phase_t is not None:
+        print("train phases (ms per iteration): " + ", ".join(
+            f"{k} {1e3 * v / args.steps:.2f}" for k, v in phase_t.items()), file=sys.stderr, flush=True)
     tot = torch.tensor([float(cells[0])], dtype=torch.float64,
                        device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
