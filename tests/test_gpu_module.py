@@ -217,6 +217,43 @@ def test_compact_rollout_equals_dense_steps(dev, graph):
     assert torch.equal(src, r)
 
 
+@pytest.mark.parametrize("case", ["all_dead", "all_live", "ragged_batch"])
+def test_compact_rollout_edge_cases(dev, case):
+    """The compact update field at its extremes: every cell dead (alpha 0: nothing packed, K2
+    reads only zeros), every cell live (alpha 1, fire 1.0: every tile row full), and a batch that
+    is not a multiple of 8 (no zig-zag K2 order); rollout == repeated dense single steps bitwise."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    m = _trained_like(dev, seed=8)
+    B = 125 if case == "ragged_batch" else 96
+    x = _state(B, 16, 72, 72, dev, seed=23)
+    if case == "all_dead":
+        x[:, 3] = 0.0
+    elif case == "all_live":
+        x[:, 3] = 1.0
+    random.seed(17)
+    offs = [random.sample(m.graph.offsets, 8) for _ in range(2)]
+    tensors = dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
+                   b1=m.update_net[0].bias, w2=m.update_net[2].weight, gn_weight=m.norm.weight,
+                   gn_bias=m.norm.bias, **m.graph.weight_tensors())
+    w, keep = S.make_weights(tensors)
+    fr = 1.0 if case == "all_live" else 0.5
+
+    def desc(t):
+        return S.make_desc(B=B, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[t],
+                           flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                           update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=fr,
+                           fire_mode=L.FIRE_HASH if fr < 1.0 else L.FIRE_NONE, rng_seed=5, rng_step=t)
+
+    assert S.rollout_compact(desc(0))
+    r = S.rollout(desc(0), w, x.contiguous(), 2, offs)
+    cur = x
+    for t in range(2):
+        cur, _ = S.step(desc(t), w, cur)
+    assert torch.equal(r, cur)
+    assert torch.isfinite(r).all()
+
+
 def test_long_rollout_drift(dev):
     """96 steps (the bench's rollout length) against the float64 oracle on the same offsets and
     hashed masks: |hip - oracle| <= 1e-4 and no alive-mask flips."""
