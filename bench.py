@@ -493,8 +493,9 @@ def main():
     fpc = flop_per_cell(wl)
     k1_flops = cells * fpc
     compact = S.rollout_compact(d)
-    # read x, write x'; read dx: dense NCHW, or on the compact field only the live cells' values
-    k2_bytes = cells * C * 4 * (2 + (live_frac if compact else 1.0))
+    # read x, write x'; read dx: dense NCHW, or on the compact field the alpha channel's dense
+    # plane and the other channels' live values only
+    k2_bytes = cells * 4 * (2 * C + (1 + (C - 1) * live_frac if compact else C))
     headline = args.config == "headline"
     # executed MFMA work per launch: live cells are packed into groups of 32 per tile (split K1,
     # v_mfma_f32_32x32x16_bf16 of 32,768 FLOP each per group: 16 channels 108 + 4 for the message,

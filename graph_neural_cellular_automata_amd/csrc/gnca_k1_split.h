@@ -155,6 +155,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
   const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
   const bool compact = a.rmask != nullptr;
+  const bool hz3 = h == 0;   // this lane half holds channel 3 (register r = 3)
   static_assert(TW <= 64, "one ballot per tile row (compact update field)");
   auto tj0 = [](int n) { return n - (n / TW) * TW; };
 
@@ -394,7 +395,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       if (compact && inb && tj0(n) == 0) a.rpre[(size_t)tile * TH + n / TW] = (uint32_t)(off + pre);
       if (live) {
         lst[off + pre] = (uint16_t)n;
-      } else if (inb && !compact && !(GNCA_ABLATE & kAblZero)) {
+      } else if (inb && compact) {   // the dense alpha plane's zero
+        a.dxa[(size_t)b * HW + cell0 + (size_t)(n / TW) * W + tj0(n)] = 0.f;
+      } else if (inb && !(GNCA_ABLATE & kAblZero)) {
         const int ti = n / TW, tj = n - (n / TW) * TW;
         float* oz = outb + (size_t)ti * W + tj;
 #pragma unroll
@@ -594,6 +597,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
             v = fmaf(fast_tanh(fmaf(bm_, S, accm[r] + accm[r + 8])), (hz && r < 4) ? 0.f : mgain, v);
           }
           if (GNCA_ABLATE & kAblStore) asm volatile("" ::"v"(v));
+          else if (compact && hz3 && r == 3) a.dxa[(size_t)b * HW + cell0 + relcell] = v;   // alpha: dense
           else ob[(size_t)((r & 3) + 8 * (r >> 2)) * cstr] = v;
           s1 += v;
           s2 = fmaf(v, v, s2);

@@ -297,7 +297,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       if (compact && inb && n % TW == 0) a.rpre[(size_t)tile * TH + n / TW] = (uint32_t)(off + pre);
       if (live) {
         lst[off + pre] = (uint16_t)n;
-      } else if (inb && !compact) {
+      } else if (inb && compact) {   // the dense alpha plane's zero
+        a.dxa[(size_t)b * HW + cell0 + (size_t)(n / TW) * W + (n % TW)] = 0.f;
+      } else if (inb) {
         const int ti = n / TW, tj = n - (n / TW) * TW;
         float* oz = outb + (size_t)ti * W + tj;
 #pragma unroll
@@ -501,7 +503,8 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
         for (int r = 0; r < 16; ++r) {
           float v = accD[r];
           if constexpr (GRAPH) v = fmaf(fast_tanh(fmaf(bmp[r], S, accm[r])), (hz && r < 4) ? 0.f : mgain, v);
-          ob[(size_t)((r & 3) + 8 * (r >> 2)) * cstr] = v;
+          if (compact && h == 0 && r == 3) a.dxa[(size_t)b * HW + cell0 + (size_t)(ti * W + tj)] = v;   // alpha: dense
+          else ob[(size_t)((r & 3) + 8 * (r >> 2)) * cstr] = v;
           s1 += v;
           s2 = fmaf(v, v, s2);
         }

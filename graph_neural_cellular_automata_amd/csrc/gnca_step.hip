@@ -154,6 +154,8 @@ struct K1Args {
   // live-cell bits, rpre[tile*TH + row] = live cells in the tile's earlier rows
   uint64_t* rmask;
   uint32_t* rpre;
+  float* dxa;          // compact mode: the alpha channel's update, dense [B,H,W] (K2 reads it over
+                       // its band's halo rows without the row tables)
   uint64_t seed;
   int64_t rng_step;
   int64_t sample_base;
@@ -1315,6 +1317,7 @@ struct K2Args {
   // compact update field (K1Args::rmask): null = dense dx; else K1's tile geometry
   const uint64_t* rmask;
   const uint32_t* rpre;
+  const float* dxa;        // dense [B,H,W] alpha-channel update (K1Args::dxa)
   int TH, TW, tiles_x;
 };
 
@@ -1358,21 +1361,14 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   float* gsh = sh_norm + 4;                          // gamma[C], then beta[C] at +32
   // compact update field (K1's rollout mode): per (band row incl. halo, K1 tile column) the row's
   // live mask, live cells before it in its tile, and the tile; per column its (tile column, column
-  // in tile).  dx of a cell = its packed value if live, else 0 (K1 multiplies dead cells by 0).
+  // in tile).  dx of a cell = its packed value if live, else 0 (K1 multiplies dead cells by 0); the
+  // alpha channel's dx is the dense plane a.dxa (the halo rows need no tables).
   constexpr bool compact = COMPACT;
   const int NCELL = a.TH * a.TW, txn = a.tiles_x;
   uint64_t* tab_m = reinterpret_cast<uint64_t*>(smem + (size_t)(2 * a.band + 2) * W);
   uint32_t* tab_p = reinterpret_cast<uint32_t*>(tab_m + (size_t)(a.band + 2) * txn);
   uint32_t* tab_t = tab_p + (size_t)(a.band + 2) * txn;
   uint32_t* colinfo = tab_t + (size_t)(a.band + 2) * txn;
-  auto dxc_at = [&](int c, int ii, int j) -> float {
-    const uint32_t ci = colinfo[j];
-    const int e = (ii - h0) * txn + (int)(ci >> 16), tj = (int)(ci & 0xffffu);
-    const uint64_t m = tab_m[e];
-    if (!((m >> tj) & 1ull)) return 0.f;
-    const uint32_t idx = tab_p[e] + (uint32_t)__popcll(m & ((1ull << tj) - 1ull));
-    return a.dx[(size_t)tab_t[e] * C * NCELL + (size_t)c * NCELL + idx];
-  };
 
   // (1) loads: gamma/beta, alpha rows, the first main items (the partials follow below; all in
   //     flight together)
@@ -1387,7 +1383,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
     if (e < na) {
       const size_t p = 3 * HW + (size_t)h0 * W + e;
       ax[u] = xb[p];
-      if (!compact) ad[u] = db[p];
+      ad[u] = compact ? a.dxa[(size_t)b * HW + (p - 3 * HW)] : db[p];
     }
   }
   if (compact) {
@@ -1448,13 +1444,6 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   __syncthreads();
   const float mu = sh_norm[0], rs = sh_norm[1];
   const float g3 = gn ? gsh[3] : 1.f, b3 = gn ? gsh[32 + 3] : 0.f;
-  if (compact) {   // the tables are in place: the alpha rows' dx and the first main items
-#pragma unroll
-    for (int u = 0; u < NA; ++u) {
-      const int e = tid + u * kThreads;
-      if (e < na) ad[u] = dxc_at(3, h0 + e / W, e - (e / W) * W);
-    }
-  }
 
   // (3) updated alpha over band + halo, then the post-update alive mask (3x3 max-pool, -inf pad)
   auto alpha_at = [&](float xa, float d) {
@@ -1468,7 +1457,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   }
   for (int e = tid + NA * kThreads; e < na; e += kThreads) {
     const size_t p = 3 * HW + (size_t)h0 * W + e;
-    at[e] = alpha_at(xb[p], compact ? dxc_at(3, h0 + e / W, e - (e / W) * W) : db[p]);
+    at[e] = alpha_at(xb[p], compact ? a.dxa[(size_t)b * HW + (p - 3 * HW)] : db[p]);
   }
   __syncthreads();
   for (int e = tid; e < nb; e += kThreads) {
@@ -1827,7 +1816,7 @@ struct Plan {
   int band_c, nbands_c, total2_c;   // K2 on the compact update field
   size_t lds2_c;
   // workspace carve (bytes)
-  size_t off_dx, off_stats, off_mm, off_offw, off_alive, off_rmask, off_rpre, ws_bytes;
+  size_t off_dx, off_stats, off_mm, off_offw, off_alive, off_rmask, off_rpre, off_dxa, ws_bytes;
   bool compact_ok;   // the rollout's compact update field (the bf16-split K1s, large batches)
 };
 
@@ -1993,6 +1982,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   }
   P->off_rmask = carve(P->compact_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint64_t) : 0);
   P->off_rpre = carve(P->compact_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint32_t) : 0);
+  P->off_dxa = carve(P->compact_ok ? (size_t)d->B * d->H * d->W * sizeof(float) : 0);
   P->ws_bytes = o;
   if (P->need_k0) {
     const size_t k0 = ((size_t)d->C * d->H + d->C + d->d_model + P->k) * sizeof(double);
@@ -2175,9 +2165,11 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   compact = compact && P.compact_ok && !active && !want_attn;
   uint64_t* rmask = reinterpret_cast<uint64_t*>(wsb + P.off_rmask);
   uint32_t* rpre = reinterpret_cast<uint32_t*>(wsb + P.off_rpre);
+  float* dxa = reinterpret_cast<float*>(wsb + P.off_dxa);
   if (compact) {
     k1.rmask = rmask;
     k1.rpre = rpre;
+    k1.dxa = dxa;
   }
   if ((phases & GNCA_PHASE_K1) && (rc = launch_k1(k1, P, st)) != GNCA_OK) return rc;
   if (!(phases & GNCA_PHASE_K2)) return GNCA_OK;
@@ -2203,6 +2195,7 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   if (compact) {
     k2.rmask = rmask;
     k2.rpre = rpre;
+    k2.dxa = dxa;
     k2.TH = P.TH;
     k2.TW = P.TW;
     k2.tiles_x = P.tiles_x;
