@@ -1967,8 +1967,9 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->compact_ok = P->var->split > 0 && P->var->TH > 0 && !msg_only && !attn_on &&
                   (long)P->total_tiles >= 2L * device_cus() * (512 / P->var->NT);
   {
-    // K2 bands on the compact field: ~12 rows (B=1024 72^2: 4 rows 0.233, 8 0.180, 12 0.170,
-    // 24 0.170 ms: the unpacking tables cost a dependent load per workgroup)
+    // K2 bands on the compact field: ~12 rows (B=1024 72^2, tables feeding the alpha rows: 4 rows
+    // 0.233, 8 0.180, 12 0.170, 24 0.170 ms; since the alpha plane is dense: 6 0.164, 8 0.158,
+    // 12 0.161, 24 0.163 ms, within the box-to-box spread)
     long rows = 12;
     static const char* band_env = getenv("GNCA_K2_BAND");   // measurement knob (A/B runs only)
     if (band_env && atoi(band_env) > 0) rows = atoi(band_env);
@@ -1979,6 +1980,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
     P->total2_c = P->nbands_c * d->B;
     P->lds2_c = (size_t)(2 * P->band_c + 2) * d->W * 4 + (size_t)(P->band_c + 2) * P->tiles_x * 16 +
                 (size_t)d->W * 4;
+    if (P->lds2_c > 64 * 1024) P->compact_ok = false;   // very wide canvases: the dense field
   }
   P->off_rmask = carve(P->compact_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint64_t) : 0);
   P->off_rpre = carve(P->compact_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint32_t) : 0);
