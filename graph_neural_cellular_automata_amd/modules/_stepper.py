@@ -46,6 +46,10 @@ class _Pack:
 
 
 _PACKS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+# fast path: the step's weight-tensor tuple and requires_grad flags -> packs; a hit skips rebuilding
+# the named list (7.5 -> 5 us per step).  A weak-keyed side table, not a module attribute: the
+# packs hold non-leaf tensors, which would break copy.deepcopy(model)
+_PACKS_FAST: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
 _SHORT_TO_NAME = {v: k for k, v in S.GRAD_FIELDS.items()}
@@ -58,6 +62,13 @@ def param_packs(model: nn.Module, tensors: dict | None = None):
     (``run_step`` has them already; walking ``named_parameters`` costs ~30 us per step).  Cached
     per module: the token only routes gradients, so it stays valid across optimiser steps as
     long as the parameter objects are the same."""
+    if tensors is not None:   # fast path: the same parameter objects and requires_grad flags
+        vals = tuple(tensors.values())
+        flags = tuple(t.requires_grad for t in vals)
+        fast = _PACKS_FAST.get(model)
+        if fast is not None and fast[0] == flags and len(fast[1]) == len(vals) and \
+                all(a is b for a, b in zip(fast[1], vals)):
+            return fast[2]
     if tensors is None:
         named = [(n, p) for n, p in model.named_parameters() if n in S.GRAD_FIELDS]
     else:
@@ -67,11 +78,15 @@ def param_packs(model: nn.Module, tensors: dict | None = None):
     hit = _PACKS.get(model)
     if hit is not None and len(hit[0]) == len(named) and all(a is b for a, (_, b) in zip(hit[0], named)) \
             and hit[2] == dev:
+        if tensors is not None:
+            _PACKS_FAST[model] = (flags, vals, hit[1])
         return hit[1]
     core = [(n, p) for n, p in named if not n.startswith("graph.")]
     graph = [(n, p) for n, p in named if n.startswith("graph.")]
     packs = (_Pack(core) if core else None, _Pack(graph) if graph else None)
     _PACKS[model] = (tuple(p for _, p in named), packs, dev)
+    if tensors is not None:
+        _PACKS_FAST[model] = (flags, vals, packs)
     return packs
 
 

@@ -86,3 +86,21 @@ def test_loss_rejects_mismatched_target():
     for ok in (torch.zeros(4, 8, 8), torch.zeros(1, 4, 8, 8), torch.zeros(3, 4, 8, 8)):
         with pytest.raises(RuntimeError, match="no CPU path"):   # shape accepted, then no CPU path
             loss_premult_rgba(pred, ok)
+
+
+def test_param_packs_fast_path_and_deepcopy():
+    """The packs' fast-path cache (weight-tensor identities + requires_grad flags) returns the
+    same packs for the same parameters, rebuilds when a flag changes, and leaves the module
+    deep-copyable (the cache is a side table, not a module attribute)."""
+    import copy
+
+    from graph_neural_cellular_automata_amd import NeuralCAGraph
+    from graph_neural_cellular_automata_amd.modules._stepper import _step_tensors, param_packs
+    m = NeuralCAGraph(16, 64)
+    a = param_packs(m, _step_tensors(m, m.graph))
+    assert param_packs(m, _step_tensors(m, m.graph)) is a
+    m.update_net[0].weight.requires_grad_(False)
+    c = param_packs(m, _step_tensors(m, m.graph))
+    assert c is not a and "update_net.0.weight" not in c[0].names
+    m2 = copy.deepcopy(m)
+    assert param_packs(m2, _step_tensors(m2, m2.graph)) is not c
