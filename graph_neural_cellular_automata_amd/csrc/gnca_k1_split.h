@@ -95,25 +95,28 @@ __host__ __device__ constexpr int ks_pstr(int rhw) {
 }
 
 struct KSLayout {
-  int xs, sp, al, kp, lst, wcnt, red, w1, bias, w2, wm, wz, bml, total;   // byte offsets
+  int xs, sp, ab, lst, cnt, cb, w1, bias, w2, wm, wz, bml, total;   // byte offsets
+  int sp_slot, lst_slot;                                             // bytes per prepared-tile slot
 };
 
 __host__ __device__ constexpr int ks_a16(int v) { return (v + 15) & ~15; }
 
+// The planes a tile's groups read besides the staged channel planes (the sender plane sp over the
+// region and the live-cell list) come in two slots: the preparer wave fills the next tile's slot
+// while the other waves still run this tile's groups (below).
 template <int TH, int TW, int RY, int RX>
 __host__ __device__ constexpr KSLayout ks_layout() {
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
-  constexpr int ALW = RW + 2, NIA = ((RH + 2) * ALW + 63) / 64;
-  constexpr int NQA = RH * (RW / 4), NIQ = (NQA + 63) / 64;
   KSLayout L{};
   int o = 0;
+  L.sp_slot = ks_a16(RHW * 4);
+  L.lst_slot = ks_a16(TH * TW * 2);
   L.xs = o; o += 16 * ks_pstr(RHW) * 4;   // first: region reads fit the 16-bit DS offsets
-  L.sp = o; o += ks_a16(RHW * 4);
-  L.al = o; o += 64 * 4 * (NIA > NIQ ? NIA : NIQ);
-  L.kp = o; o += ks_a16(TH * TW);
-  L.lst = o; o += ks_a16(TH * TW * 2);
-  L.wcnt = o; o += 32;
-  L.red = o; o += 256;
+  L.sp = o; o += 2 * L.sp_slot;           // sender plane (floats), two slots
+  L.ab = o; o += ks_a16(RHW);             // the preparer's alive bytes over the region
+  L.lst = o; o += 2 * L.lst_slot;         // live-cell list (u16 cell indices), two slots
+  L.cnt = o; o += 16;                     // live cells per slot
+  L.cb = o; o += ks_a16(8 * (TH * TW / 64 + 2));   // the preparer's 64-cell chunk ballots
   L.w1 = o; o += 3 * 4 * 3 * 1024;       // [plane][rb][kc][lane] x 16 B
   L.bias = o; o += 4 * 32 * 16;          // [rb][row] x 16 B (k slots 0..2 = the three parts)
   L.w2 = o; o += 3 * 8 * 2 * 16 * 16;    // [plane][s][h][channel] x 16 B
@@ -131,33 +134,32 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
   constexpr int PSTR = ks_pstr(RHW);
   constexpr int NQ = RHW / 4, NI4 = (NQ + 63) / 64;
-  constexpr int ALW = RW + 2, NIA = ((RH + 2) * ALW + 63) / 64;
-  constexpr int QW = RW / 4, NQA = RH * QW, NIQ = (NQA + 63) / 64;
+  constexpr int QW = RW / 4, NQA = RH * QW;
   constexpr int NCELL = TH * TW;
   constexpr KSLayout L = ks_layout<TH, TW, RY, RX>();
   static_assert(RW % 4 == 0 && RX % 4 == 0 && TW % 4 == 0, "16-byte staging rows");
   static_assert(RY >= 1 && RX >= 1, "perception halo");
   static_assert(L.total <= 160 * 1024, "LDS");
   static_assert(7 * PSTR * 4 + 4 * RHW < 65536, "channel offsets fit the DS immediate");
+  static_assert(TW <= 64, "one ballot per tile row (compact update field)");
   constexpr bool GRAPH = KU > 0;
+  // The preparer is wave 3, the OLDER wave of SIMD 3 (waves w and w + 4 share SIMD w; the younger
+  // one gets the leftover issue slots).  Groups go to waves by slot (q = slot, slot + 8, ...) with
+  // waves 3 and 7 on the last two slots, so SIMD 3 runs the fewest groups beside the preparation.
+  constexpr int PW = 3;
 
   float* xs = reinterpret_cast<float*>(smem_b + L.xs);
-  float* sp = reinterpret_cast<float*>(smem_b + L.sp);
-  float* al = reinterpret_cast<float*>(smem_b + L.al);
-  uint8_t* kp = reinterpret_cast<uint8_t*>(smem_b + L.kp);
-  uint16_t* lst = reinterpret_cast<uint16_t*>(smem_b + L.lst);
-  int* wcnt = reinterpret_cast<int*>(smem_b + L.wcnt);
+  int* cnt = reinterpret_cast<int*>(smem_b + L.cnt);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31, c16 = lane & 15;
+  const int gslot = wave < 3 ? wave : (wave == 3 ? 7 : (wave == 7 ? 6 : wave - 1));
   const int H = a.H, W = a.W;
   const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
-  const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
   const bool compact = a.rmask != nullptr;
   const bool hz3 = h == 0;   // this lane half holds channel 3 (register r = 3)
-  static_assert(TW <= 64, "one ballot per tile row (compact update field)");
-  auto tj0 = [](int n) { return n - (n / TW) * TW; };
+  const size_t HW = (size_t)H * W;
 
   // ---- weight images (bf16 parts in MFMA fragment order), once per persistent workgroup ----
   if (!(GNCA_ABLATE & kAblFill)) {
@@ -220,6 +222,148 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
     // the perception zero tap: every channel plane's pad floats (never written by the staging)
     for (int e = tid; e < 16 * (PSTR - RHW); e += NT) xs[(e / (PSTR - RHW)) * PSTR + RHW + e % (PSTR - RHW)] = 0.f;
   }
+
+  // XCD-aware tile order (as gnca_k1_update)
+  const int nxcd = gridDim.x >= 8 ? 8 : 1;
+  const int xg_ = blockIdx.x % nxcd, xr_ = blockIdx.x / nxcd;
+  const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
+  const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
+  const int t_begin = xg_ * tq + min(xg_, trm), t_end = (GNCA_ABLATE & kAblTiles) ? t_begin : t_begin + tq + (xg_ < trm ? 1 : 0);
+
+  // the next active tile of this workgroup's sequence after `t` (inactive samples of a masked step
+  // get zero GroupNorm partials and no work)
+  auto next_active = [&](int t) {
+    while (t < t_end && a.active && !a.active[t / a.tps]) {
+      if (tid < 2 * NW) a.stats[(size_t)t * 2 * NW + tid] = 0.0;
+      t += per_x;
+    }
+    return t;
+  };
+
+  // LDS-DMA staging of a tile's channel planes: 16-byte quads of every plane (torus-wrapped), lanes
+  // past the region masked off (the plane pads stay zero)
+  auto issue_dma = [&](int t) {
+    const int b = t / a.tps, tin = t - b * a.tps;
+    const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+    const int i0 = ty * TH, j0 = tx * TW;
+    const float* xb = a.x + (size_t)b * C * HW;
+#pragma unroll 1
+    for (int ii_ = wave; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI4); ii_ += NW) {
+      const int q = 64 * ii_ + lane;
+      if (q < NQ) {
+        const int e = 4 * q, vr = e / RW, vc = e - (e / RW) * RW;
+        int ii = i0 - RY + vr, jj = j0 - RX + vc;
+        ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
+        jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
+        const float* src0 = xb + ii * W + jj;
+        float* dst = xs + 256 * ii_;
+#pragma unroll 4
+        for (int c = 0; c < C; ++c)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (size_t)c * HW),
+                                           (__attribute__((address_space(3))) void*)(dst + c * PSTR), 16, 0, 0);
+      }
+    }
+  };
+
+  // The preparer (one wave, no workgroup barrier): a tile's sender plane over the region, its keep
+  // mask (fire AND pre-alive) and live-cell list into slot `s`; the compact field's row tables and
+  // the dead cells' zeros go to global memory.  The pre-update masks are the alive bytes (K2's
+  // hand-over in a rollout, else gnca_k_alive over this step's alpha plane).
+  auto prep = [&](int t, int s) {
+    const int b = t / a.tps, tin = t - b * a.tps;
+    const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+    const int i0 = ty * TH, j0 = tx * TW;
+    const size_t cell0 = (size_t)i0 * W + j0;
+    float* spp = reinterpret_cast<float*>(smem_b + L.sp + s * L.sp_slot);
+    uint16_t* lstp = reinterpret_cast<uint16_t*>(smem_b + L.lst + s * L.lst_slot);
+    uint32_t* abw = reinterpret_cast<uint32_t*>(smem_b + L.ab);
+    const uint8_t* abq = reinterpret_cast<const uint8_t*>(smem_b + L.ab);
+    uint64_t* cb = reinterpret_cast<uint64_t*>(smem_b + L.cb);
+    // (1) the region's alive bytes, 4 columns per dword, all loads in flight together
+    {
+      const uint8_t* alb = a.alive + (size_t)b * HW;
+      constexpr int NU = (NQA + 63) / 64;
+      uint32_t v[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int e = 64 * u + lane;
+        v[u] = 0u;
+        if (e < NQA) {
+          const int vr = e / QW, vc = 4 * (e - (e / QW) * QW);
+          int ii = i0 - RY + vr, jj = j0 - RX + vc;
+          ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
+          jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
+          v[u] = *reinterpret_cast<const uint32_t*>(alb + ii * W + jj);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int e = 64 * u + lane;
+        if (e < NQA) {
+          abw[e] = v[u];
+          if constexpr (GRAPH) {
+            f4 q;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = a2a ? (float)((v[u] >> (8 * k + 1)) & 1u) : 1.f;
+            *reinterpret_cast<f4*>(spp + 4 * e) = q;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // (2) keep = fire AND pre-alive per 64-cell chunk; live cells listed in cell order
+    float* outb = a.out + (size_t)b * C * HW + cell0;
+    int nl = 0;
+#pragma unroll 1
+    for (int n0 = 0; n0 < NCELL; n0 += 64) {
+      const int n = n0 + lane;
+      const bool inb = n < NCELL;
+      const int ti = n / TW, tj = n - (n / TW) * TW;
+      const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
+      bool live = false;
+      if (inb && (abq[(ti + RY) * RW + tj + RX] & 1u))
+        live = (GNCA_ABLATE & kAblFire) ? ((cell & 1) != 0)
+                                        : fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step,
+                                                  a.sample_base, b, HW, cell);
+      const uint64_t bal = __ballot(live);
+      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) cb[n0 >> 6] = bal;
+      if (compact && inb && tj == 0) a.rpre[(size_t)t * TH + ti] = (uint32_t)(nl + pre);
+      if (live) {
+        lstp[nl + pre] = (uint16_t)n;
+      } else if (inb && compact) {   // the dense alpha plane's zero
+        a.dxa[(size_t)b * HW + cell0 + (size_t)ti * W + tj] = 0.f;
+      } else if (inb && !(GNCA_ABLATE & kAblZero)) {
+        float* oz = outb + (size_t)ti * W + tj;
+#pragma unroll
+        for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
+      }
+      nl += __popcll(bal);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // (3) per-row live masks of the compact update field, from the chunk ballots
+    if (compact) {
+#pragma unroll 1
+      for (int ti = lane; ti < TH; ti += 64) {
+        const int f = ti * TW, c0 = f >> 6, sh = f & 63;
+        uint64_t m = cb[c0] >> sh;
+        if (sh + TW > 64) m |= cb[c0 + 1] << (64 - sh);
+        if (TW < 64) m &= (1ull << TW) - 1ull;
+        a.rmask[(size_t)t * TH + ti] = m;
+      }
+    }
+    if (lane == 0) cnt[s] = nl;
+  };
+
+  PROF_DECL
+  int tile = next_active(t_begin + xr_);
+  if (tile < t_end) issue_dma(tile);
+  if (wave == PW && tile < t_end) prep(tile, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch; the
   // other case reads the weights from global memory, an uncommon slow path)
   int ok = 1;
@@ -231,7 +375,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
     else ref = (float)((tr == 0 ? 1 : (tr == 2 ? -1 : 0)) * (tc == 1 ? 2 : 1));
     if (a.perc[idx] != ref) ok = 0;
   }
-  const bool sobel = __syncthreads_and(ok) != 0;   // also the barrier after the image stores
+  const bool sobel = __syncthreads_and(ok) != 0;   // also the barrier after the images, DMA and prep
 
   // per-lane LDS offsets of the message fragments (stacks [M0;M1], [M2;0], [M0;0], read per
   // group: kept out of the registers the group loop needs) and of the message bias of this lane's 8
@@ -249,179 +393,28 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   const int w2T0 = L.w2 + (r32 < 16 ? 0 : 4096) + (h * 16 + c16) * 16;
   const int w2T1 = L.w2 + 8192 + (h * 16 + c16) * 16;
 
-  const size_t HW = (size_t)H * W;
-
-  // XCD-aware tile order (as gnca_k1_update)
-  const int nxcd = gridDim.x >= 8 ? 8 : 1;
-  const int xg_ = blockIdx.x % nxcd, xr_ = blockIdx.x / nxcd;
-  const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
-  const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
-  const int t_begin = xg_ * tq + min(xg_, trm), t_end = t_begin + tq + (xg_ < trm ? 1 : 0);
-  PROF_DECL
-  for (int tile = t_begin + xr_; tile < ((GNCA_ABLATE & kAblTiles) ? t_begin : t_end); tile += per_x) {
-    PROF_MARK(7);   // loop back-edge / tail of the previous tile
+  // Tile pipeline: [groups of tile t | the preparer then fills slot par^1 for tile t+1] -> barrier
+  // -> LDS-DMA of tile t+1's channel planes -> wait -> barrier.  The per-tile planes and the
+  // compaction run on the preparer wave beside the other waves' groups instead of between them.
+  int par = 0;
+  while (tile < t_end) {
+    PROF_MARK(7);
+    const int nxt = next_active(tile + per_x);
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
-    const float* xb = a.x + (size_t)b * C * HW;
-    if (a.active && !a.active[b]) {   // inactive sample (masked step)
-      if (tid < 2 * NW) a.stats[(size_t)tile * 2 * NW + tid] = 0.0;
-      continue;
-    }
-    __syncthreads();   // the previous tile's LDS readers are done
-    PROF_MARK(6);   // top barrier (waiting for the slowest wave of the previous tile)
-
-    // ---- LDS-DMA staging: 16-byte quads of every channel plane (torus-wrapped), lanes past the
-    //      region masked off (the plane pads stay zero) ----
-#pragma unroll 1
-    for (int ii_ = wave; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI4); ii_ += NW) {
-      const int q = 64 * ii_ + lane;
-      if (q < NQ) {
-        const int e = 4 * q, vr = e / RW, vc = e - (e / RW) * RW;
-        int ii = i0 - RY + vr, jj = j0 - RX + vc;
-        ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
-        jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-        const float* src0 = xb + ii * W + jj;
-        float* dst = xs + 256 * ii_;
-#pragma unroll 4
-        for (int c = 0; c < C; ++c)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (size_t)c * HW),
-                                           (__attribute__((address_space(3))) void*)(dst + c * PSTR), 16, 0, 0);
-      }
-    }
-    if (a.alive) {
-      // the previous K2's alive bytes over the region, one dword = 4 columns
-      const uint8_t* ab = a.alive + (size_t)b * HW;
-#pragma unroll 1
-      for (int ii_ = wave; ii_ < NIQ; ii_ += NW) {
-        const int e = 64 * ii_ + lane;
-        int off = 0;
-        if (e < NQA) {
-          const int vr = e / QW, vc = 4 * (e - (e / QW) * QW);
-          int ii = i0 - RY + vr, jj = j0 - RX + vc;
-          ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
-          jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-          off = ii * W + jj;
-        }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ab + off),
-                                         (__attribute__((address_space(3))) void*)(al + 64 * ii_), 4, 0, 0);
-      }
-    } else {
-      // alpha plane with one more ring: element e of ((RH+2) x ALW) -> (i0-RY-1+vr, j0-RX-1+vc)
-#pragma unroll 1
-      for (int ii_ = wave; ii_ < NIA; ii_ += NW) {
-        const int e = 64 * ii_ + lane;
-        int off = 0;
-        if (e < (RH + 2) * ALW) {
-          const int vr = e / ALW, vc = e - (e / ALW) * ALW;
-          int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
-          while (ii < 0) ii += H;
-          while (ii >= H) ii -= H;
-          while (jj < 0) jj += W;
-          while (jj >= W) jj -= W;
-          off = ii * W + jj;
-        }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xb + 3 * HW + off),
-                                         (__attribute__((address_space(3))) void*)(al + 64 * ii_), 4, 0, 0);
-      }
-    }
-    PROF_MARK(0);   // DMA issue
-    // ---- fire plane while the DMA is in flight ----
-#pragma unroll 1
-    for (int n = tid; n < NCELL; n += NT) {
-      const int ti = n / TW, tj = n - (n / TW) * TW;
-      const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
-      kp[n] = ((GNCA_ABLATE & kAblFire) ? ((cell & 1) != 0)
-                                        : fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step,
-                                                  a.sample_base, b, HW, cell)) ? 1 : 0;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    PROF_MARK(1);   // fire plane + DMA wait + barrier
-
-    // ---- sender plane over the region, keep = pre-alive AND fire over the tile ----
-    if (a.alive) {
-      const uint8_t* alb = reinterpret_cast<const uint8_t*>(al);
-#pragma unroll 1
-      for (int pos = tid; pos < ((GNCA_ABLATE & kAblPlanes) ? 0 : RHW); pos += NT) {
-        const int vr = pos / RW, vc = pos - (pos / RW) * RW;
-        const int v = alb[pos];
-        sp[pos] = a2a ? (float)((v >> 1) & 1) : 1.f;
-        const int ti = vr - RY, tj = vc - RX;
-        if (ti >= 0 && ti < TH && tj >= 0 && tj < TW && !(v & 1)) kp[ti * TW + tj] = 0;
-      }
-    } else {
-#pragma unroll 1
-      for (int pos = tid; pos < RHW; pos += NT) {
-        const int vr = pos / RW, vc = pos - (pos / RW) * RW;
-        int iq = i0 - RY + vr, jq = j0 - RX + vc;
-        while (iq < 0) iq += H;
-        while (iq >= H) iq -= H;
-        while (jq < 0) jq += W;
-        while (jq >= W) jq -= W;
-        const float* q = al + (vr + 1) * ALW + (vc + 1);
-        const float NEG = -INFINITY;
-        const bool up = iq > 0, dn = iq < H - 1, lf = jq > 0, rt = jq < W - 1;
-        const float mu_ = fmaxf(fmaxf(lf ? q[-ALW - 1] : NEG, q[-ALW]), rt ? q[-ALW + 1] : NEG);
-        const float mm_ = fmaxf(fmaxf(lf ? q[-1] : NEG, q[0]), rt ? q[1] : NEG);
-        const float md_ = fmaxf(fmaxf(lf ? q[ALW - 1] : NEG, q[ALW]), rt ? q[ALW + 1] : NEG);
-        const float mx = fmaxf(fmaxf(up ? mu_ : NEG, mm_), dn ? md_ : NEG);
-        sp[pos] = a2a ? (mx > gthr ? 1.f : 0.f) : 1.f;
-        const int ti = vr - RY, tj = vc - RX;
-        if (ti >= 0 && ti < TH && tj >= 0 && tj < TW && !(mx > thr)) kp[ti * TW + tj] = 0;
-      }
-    }
-    __syncthreads();
-    PROF_MARK(2);   // planes + barrier
-
-    // ---- live-cell compaction (cell order, wave ballots: deterministic); dead cells get dx = 0 ----
     const size_t cell0 = (size_t)i0 * W + j0;
     float* outb = a.out + (size_t)b * C * HW + cell0;
-    int nlive = 0;
-    for (int n0 = 0; n0 < NCELL; n0 += NT) {
-      const int n = n0 + tid;
-      const bool inb = n < NCELL;
-      const bool live = inb && kp[n] != 0;
-      const uint64_t bal = __ballot(live);
-      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-      if (lane == 0) wcnt[wave] = __popcll(bal);
-      __syncthreads();
-      int off = nlive, tot = 0;
-#pragma unroll
-      for (int w_ = 0; w_ < NW; ++w_) {
-        off += w_ < wave ? wcnt[w_] : 0;
-        tot += wcnt[w_];
-      }
-      if (compact && inb && tj0(n) == 0) a.rpre[(size_t)tile * TH + n / TW] = (uint32_t)(off + pre);
-      if (live) {
-        lst[off + pre] = (uint16_t)n;
-      } else if (inb && compact) {   // the dense alpha plane's zero
-        a.dxa[(size_t)b * HW + cell0 + (size_t)(n / TW) * W + tj0(n)] = 0.f;
-      } else if (inb && !(GNCA_ABLATE & kAblZero)) {
-        const int ti = n / TW, tj = n - (n / TW) * TW;
-        float* oz = outb + (size_t)ti * W + tj;
-#pragma unroll
-        for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
-      }
-      nlive += tot;
-      __syncthreads();   // wcnt is rewritten by the next pass
-    }
-
-    if (compact) {   // per-row live masks of the compact update field (one ballot per tile row)
-#pragma unroll 1
-      for (int ti = wave; ti < TH; ti += NW) {
-        const uint64_t m = __ballot(lane < TW && kp[ti * TW + (lane < TW ? lane : 0)] != 0);
-        if (lane == 0) a.rmask[(size_t)tile * TH + ti] = m;
-      }
-    }
-    PROF_MARK(3);   // compaction
+    const float* sp = reinterpret_cast<const float*>(smem_b + L.sp + par * L.sp_slot);
+    const uint16_t* lst = reinterpret_cast<const uint16_t*>(smem_b + L.lst + par * L.lst_slot);
+    const int nlive = cnt[par];
 
     // ---- 32-cell groups ----
     float s1 = 0.f, s2 = 0.f;
     const int qend = (nlive + 31) >> 5;
     const bool img_top = i0 == 0, img_bot = i0 + TH == H, img_lft = j0 == 0, img_rgt = j0 + TW == W;
 #pragma unroll 1
-    for (int q = wave; q < qend; q += NW) {
+    for (int q = gslot; q < qend; q += NW) {
       const int gi = 32 * q + r32;
       const bool valid = gi < nlive;
       const int n = lst[valid ? gi : 0];
@@ -606,20 +599,34 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
     }
 
     PROF_MARK(4);   // group loop
+    if (wave == PW && nxt < t_end) prep(nxt, par ^ 1);
+    PROF_MARK(3);   // preparer
     // ---- per-(tile, wave) GroupNorm partials (fp64 wave shuffle; K2 sums them in fixed order) ----
-    if (GNCA_ABLATE & kAblReduce) continue;
-    double d1 = s1, d2 = s2;
-    for (int off = 32; off > 0; off >>= 1) {
-      d1 += __shfl_xor(d1, off);
-      d2 += __shfl_xor(d2, off);
-    }
-    if (lane == 0) {
-      a.stats[((size_t)tile * NW + wave) * 2 + 0] = d1;
-      a.stats[((size_t)tile * NW + wave) * 2 + 1] = d2;
+    if (!(GNCA_ABLATE & kAblReduce)) {
+      double d1 = s1, d2 = s2;
+      for (int off = 32; off > 0; off >>= 1) {
+        d1 += __shfl_xor(d1, off);
+        d2 += __shfl_xor(d2, off);
+      }
+      if (lane == 0) {
+        a.stats[((size_t)tile * NW + wave) * 2 + 0] = d1;
+        a.stats[((size_t)tile * NW + wave) * 2 + 1] = d2;
+      }
     }
     PROF_MARK(5);   // per-tile reduction
+    if (nxt < t_end) {
+      __syncthreads();   // this tile's groups are done with the staged planes; slot par^1 is ready
+      PROF_MARK(6);
+      issue_dma(nxt);
+      PROF_MARK(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      PROF_MARK(1);
+    }
+    tile = nxt;
+    par ^= 1;
   }
-  PROF_STORE_W04;
+  PROF_STORE_W03;
 }
 
 }  // namespace gnca

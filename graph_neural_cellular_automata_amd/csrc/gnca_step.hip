@@ -71,7 +71,10 @@ __device__ unsigned long long g_prof[1024][2 * kProfPhases];   // [.][8..15]: sp
 #define PROF_STORE do { if (threadIdx.x == 0) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][i_] = prof_acc[i_]; } while (0)
 // waves 0 and 4 (the two waves of SIMD 0): [.][0..7] and [.][8..15]
 #define PROF_STORE_W04 do { if ((threadIdx.x & 255) == 0) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][(threadIdx.x >> 8) * kProfPhases + i_] = prof_acc[i_]; } while (0)
+// waves 0 and 3 (the split K1's preparer): [.][0..7] and [.][8..15]
+#define PROF_STORE_W03 do { if (threadIdx.x == 0 || threadIdx.x == 192) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][(threadIdx.x ? kProfPhases : 0) + i_] = prof_acc[i_]; } while (0)
 #else
+#define PROF_STORE_W03 do {} while (0)
 #define PROF_STORE_W04 do {} while (0)
 #define PROF_DECL
 #define PROF_MARK(i) do {} while (0)
@@ -1591,6 +1594,27 @@ __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
   k2_body<V, COMPACT>(a, smem, sh_norm);
 }
 
+// This step's pre-update masks as bytes for the split K1 when no previous K2 handed them over
+// (single steps, the first step of a rollout): bit 0 = maxpool3(alpha) > alpha_thr, bit 1 =
+// > graph_alpha_thr (ncagraph.py:85-92: -inf padding, no wrap), the bytes K2 writes in a rollout.
+__global__ __launch_bounds__(kThreads) void gnca_k_alive(const float* x, uint8_t* out, int B, int C, int H, int W,
+                                                         float thr, float gthr) {
+  const size_t HW = (size_t)H * W, n = (size_t)B * HW;
+  for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (size_t)gridDim.x * kThreads) {
+    const size_t b = i / HW;
+    const int p = (int)(i - b * HW), r = p / W, c = p - (p / W) * W;
+    const float* al = x + (b * C + 3) * HW;
+    float mx = -INFINITY;
+    for (int ii = max(0, r - 1); ii <= min(H - 1, r + 1); ++ii) {
+      const float* row = al + (size_t)ii * W;
+      mx = fmaxf(mx, row[c]);
+      if (c > 0) mx = fmaxf(mx, row[c - 1]);
+      if (c < W - 1) mx = fmaxf(mx, row[c + 1]);
+    }
+    out[i] = (uint8_t)((mx > thr ? 1 : 0) | (mx > gthr ? 2 : 0));
+  }
+}
+
 // normalise a message-only attention map (no K2 in message mode)
 __global__ __launch_bounds__(kThreads) void gnca_attn_normalize(float* attn, const float* attn_mm,
                                                                 int tps, int HW) {
@@ -2162,7 +2186,17 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   fill_k1(k1, d, w, P, x, dx, fire, want_attn ? attn : nullptr, wsb);
   k1.active = active;
   uint8_t* alive = reinterpret_cast<uint8_t*>(wsb + P.off_alive);
-  k1.alive = alive_in ? alive : nullptr;
+  // the 16-channel split K1 always reads the masks as bytes (its preparer wave builds the planes
+  // from them): without a hand-over from the previous K2, gnca_k_alive makes them first
+  const bool bytes_k1 = P.var->split == 1;
+  k1.alive = (alive_in || bytes_k1) ? alive : nullptr;
+  if ((phases & GNCA_PHASE_K1) && bytes_k1 && !alive_in) {
+    const size_t cells = (size_t)d->B * d->H * d->W;
+    const unsigned g = (unsigned)std::min<size_t>((cells + kThreads - 1) / kThreads, 4096);
+    hipLaunchKernelGGL(gnca_k_alive, dim3(g), dim3(kThreads), 0, st, x, alive, d->B, d->C, d->H, d->W,
+                       d->alpha_thr, d->graph_alpha_thr);
+    if ((rc = check_launch()) != GNCA_OK) return rc;
+  }
   // compact update field (rollout mode): K1 packs the live cells' dx per tile, K2 unpacks them
   compact = compact && P.compact_ok && !active && !want_attn;
   uint64_t* rmask = reinterpret_cast<uint64_t*>(wsb + P.off_rmask);

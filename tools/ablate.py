@@ -114,7 +114,12 @@ def run(reps=15, rounds=3):
     import numpy as np
     full = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16).astype(np.float64)
     ws = full[:, 8:].sum() > 0
-    if os.environ.get("ABLATE_PROF_SETS") == "w04":   # the split K1: both waves of SIMD 0
+    if os.environ.get("ABLATE_PROF_SETS") == "w03":   # the split K1: wave 0 and the preparer wave 3
+        names = ["dma_issue", "dma_wait+barrier", "-", "preparer", "groups", "reduction",
+                 "barrier_before_dma", "loop_top"]
+        sets = [("wave 0 (SIMD 0, older)", names, full[:, :8]),
+                ("wave 3 (SIMD 3, preparer)", names, full[:, 8:])]
+    elif os.environ.get("ABLATE_PROF_SETS") == "w04":   # the split K1: both waves of SIMD 0
         names = ["dma_issue", "fire+dma_wait", "planes", "compaction", "groups", "reduction",
                  "top_barrier", "loop_tail"]
         sets = [("wave 0 (SIMD 0, older)", names, full[:, :8]),
