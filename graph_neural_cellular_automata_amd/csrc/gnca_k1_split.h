@@ -95,7 +95,7 @@ __host__ __device__ constexpr int ks_pstr(int rhw) {
 }
 
 struct KSLayout {
-  int xs, sp, ab, lst, cnt, cb, w1, bias, w2, wm, wz, bml, total;   // byte offsets
+  int xs, sp, ab, lst, cnt, cb, pg, w1, bias, w2, wm, wz, bml, total;   // byte offsets
   int sp_slot, lst_slot;                                             // bytes per prepared-tile slot
 };
 
@@ -115,8 +115,9 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   L.sp = o; o += 2 * L.sp_slot;           // sender plane (floats), two slots
   L.ab = o; o += ks_a16(RHW);             // the preparer's alive bytes over the region
   L.lst = o; o += 2 * L.lst_slot;         // live-cell list (u16 cell indices), two slots
-  L.cnt = o; o += 16;                     // live cells per slot
+  L.cnt = o; o += 16;                     // live cells per slot; the group counter
   L.cb = o; o += ks_a16(8 * (TH * TW / 64 + 2));   // the preparer's 64-cell chunk ballots
+  L.pg = o; o += 16 * ((TH * TW + 31) / 32);     // per-group GroupNorm partials (fp64 pairs)
   L.w1 = o; o += 3 * 4 * 3 * 1024;       // [plane][rb][kc][lane] x 16 B
   L.bias = o; o += 4 * 32 * 16;          // [rb][row] x 16 B (k slots 0..2 = the three parts)
   L.w2 = o; o += 3 * 8 * 2 * 16 * 16;    // [plane][s][h][channel] x 16 B
@@ -125,6 +126,23 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   L.bml = o; o += 2 * 8 * 4;             // message bias per (lane half h, accumulator register r)
   L.total = o;
   return L;
+}
+
+// The next group of a tile: one LDS add by the whole wave (the counter moves by 64 per pull, so
+// the old value >> 6 is the group).  Inline asm: the compiler would otherwise treat the atomic as
+// possibly aliasing the in-flight LDS-DMA staging and wait for every outstanding memory operation
+// (the previous group's dx stores) first; the counter is never a DMA destination.
+#ifndef GNCA_K1_PULL
+#define GNCA_K1_PULL 1   // A/B builds only: 0 static (q = wave, wave + 8, ...), 2 inline-asm add (measured B=1024: 0.515, 0.460 (1), 0.470 ms)
+#endif
+__device__ __forceinline__ int pull_group(int* ctr) {
+  int old;
+  const int one = 1;
+  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(old)
+               : "v"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)ctr), "v"(one)
+               : "memory");
+  return __builtin_amdgcn_readfirstlane(old) >> 6;
 }
 
 template <int TH, int TW, int RY, int RX, int KU>
@@ -144,16 +162,16 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   static_assert(TW <= 64, "one ballot per tile row (compact update field)");
   constexpr bool GRAPH = KU > 0;
   // The preparer is wave 3, the OLDER wave of SIMD 3 (waves w and w + 4 share SIMD w; the younger
-  // one gets the leftover issue slots).  Groups go to waves by slot (q = slot, slot + 8, ...) with
-  // waves 3 and 7 on the last two slots, so SIMD 3 runs the fewest groups beside the preparation.
+  // one gets the leftover issue slots): it prepares the next tile first, then joins the groups.
   constexpr int PW = 3;
 
   float* xs = reinterpret_cast<float*>(smem_b + L.xs);
   int* cnt = reinterpret_cast<int*>(smem_b + L.cnt);
+  int* gctr = cnt + 2;   // next group of the tile (LDS atomic)
+  double* pg = reinterpret_cast<double*>(smem_b + L.pg);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31, c16 = lane & 15;
-  const int gslot = wave < 3 ? wave : (wave == 3 ? 7 : (wave == 7 ? 6 : wave - 1));
   const int H = a.H, W = a.W;
   const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
@@ -333,9 +351,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       if (compact && inb && tj == 0) a.rpre[(size_t)t * TH + ti] = (uint32_t)(nl + pre);
       if (live) {
         lstp[nl + pre] = (uint16_t)n;
-      } else if (inb && compact) {   // the dense alpha plane's zero
-        a.dxa[(size_t)b * HW + cell0 + (size_t)ti * W + tj] = 0.f;
-      } else if (inb && !(GNCA_ABLATE & kAblZero)) {
+      } else if (inb && !compact && !(GNCA_ABLATE & kAblZero)) {   // (compact: K2 masks by the row tables)
         float* oz = outb + (size_t)ti * W + tj;
 #pragma unroll
         for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
@@ -363,6 +379,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   int tile = next_active(t_begin + xr_);
   if (tile < t_end) issue_dma(tile);
   if (wave == PW && tile < t_end) prep(tile, 0);
+  if (tid == 0) *gctr = 0;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch; the
   // other case reads the weights from global memory, an uncommon slow path)
@@ -409,12 +426,25 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
     const uint16_t* lst = reinterpret_cast<const uint16_t*>(smem_b + L.lst + par * L.lst_slot);
     const int nlive = cnt[par];
 
-    // ---- 32-cell groups ----
-    float s1 = 0.f, s2 = 0.f;
+    if (wave == PW && nxt < t_end) prep(nxt, par ^ 1);
+    PROF_MARK(3);   // preparer
+
+    // ---- 32-cell groups, pulled from an LDS counter (the faster, older wave of a SIMD takes more);
+    //      each group's GroupNorm partials go to pg[q], so the sums do not depend on which wave ran it ----
     const int qend = (nlive + 31) >> 5;
     const bool img_top = i0 == 0, img_bot = i0 + TH == H, img_lft = j0 == 0, img_rgt = j0 + TW == W;
 #pragma unroll 1
-    for (int q = gslot; q < qend; q += NW) {
+    // (every lane adds 1: the wave's 64 increments are one LDS instruction, so the counter moves by
+    //  64 per pull and any lane's old value >> 6 is the pulled group)
+#if GNCA_K1_PULL == 0
+    for (int q = wave; q < qend; q += NW) {
+#elif GNCA_K1_PULL == 1
+    for (int q = __builtin_amdgcn_readfirstlane(atomicAdd(gctr, 1)) >> 6; q < qend;
+         q = __builtin_amdgcn_readfirstlane(atomicAdd(gctr, 1)) >> 6) {
+#else
+    for (int q = pull_group(gctr); q < qend; q = pull_group(gctr)) {
+#endif
+      float s1 = 0.f, s2 = 0.f;
       const int gi = 32 * q + r32;
       const bool valid = gi < nlive;
       const int n = lst[valid ? gi : 0];
@@ -596,27 +626,32 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
           s2 = fmaf(v, v, s2);
         }
       }
+      if (!(GNCA_ABLATE & kAblReduce)) {
+        double d1 = s1, d2 = s2;
+        for (int off = 32; off > 0; off >>= 1) {
+          d1 += __shfl_xor(d1, off);
+          d2 += __shfl_xor(d2, off);
+        }
+        if (lane == 0) {
+          pg[2 * q] = d1;
+          pg[2 * q + 1] = d2;
+        }
+      }
     }
 
     PROF_MARK(4);   // group loop
-    if (wave == PW && nxt < t_end) prep(nxt, par ^ 1);
-    PROF_MARK(3);   // preparer
-    // ---- per-(tile, wave) GroupNorm partials (fp64 wave shuffle; K2 sums them in fixed order) ----
-    if (!(GNCA_ABLATE & kAblReduce)) {
-      double d1 = s1, d2 = s2;
-      for (int off = 32; off > 0; off >>= 1) {
-        d1 += __shfl_xor(d1, off);
-        d2 += __shfl_xor(d2, off);
-      }
-      if (lane == 0) {
-        a.stats[((size_t)tile * NW + wave) * 2 + 0] = d1;
-        a.stats[((size_t)tile * NW + wave) * 2 + 1] = d2;
-      }
+    __syncthreads();   // this tile's groups are done (staged planes free, pg complete, slot par^1 ready)
+    PROF_MARK(6);
+    if (tid == 0) *gctr = 0;
+    // ---- the tile's GroupNorm partials in 8 bins (bin j: groups j, j + 8, ... in order; K2 sums the
+    //      bins of a sample in fixed order) ----
+    if (tid < 2 * NW) {
+      double s_ = 0.0;
+      for (int q = tid >> 1; q < qend; q += NW) s_ += pg[2 * q + (tid & 1)];
+      a.stats[(size_t)tile * 2 * NW + tid] = s_;
     }
     PROF_MARK(5);   // per-tile reduction
     if (nxt < t_end) {
-      __syncthreads();   // this tile's groups are done with the staged planes; slot par^1 is ready
-      PROF_MARK(6);
       issue_dma(nxt);
       PROF_MARK(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

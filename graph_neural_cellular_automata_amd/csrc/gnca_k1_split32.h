@@ -297,9 +297,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       if (compact && inb && n % TW == 0) a.rpre[(size_t)tile * TH + n / TW] = (uint32_t)(off + pre);
       if (live) {
         lst[off + pre] = (uint16_t)n;
-      } else if (inb && compact) {   // the dense alpha plane's zero
-        a.dxa[(size_t)b * HW + cell0 + (size_t)(n / TW) * W + (n % TW)] = 0.f;
-      } else if (inb) {
+      } else if (inb && !compact) {   // (compact: K2 masks the alpha plane by the row tables)
         const int ti = n / TW, tj = n - (n / TW) * TW;
         float* oz = outb + (size_t)ti * W + tj;
 #pragma unroll

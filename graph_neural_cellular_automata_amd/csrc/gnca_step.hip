@@ -157,7 +157,7 @@ struct K1Args {
   // live-cell bits, rpre[tile*TH + row] = live cells in the tile's earlier rows
   uint64_t* rmask;
   uint32_t* rpre;
-  float* dxa;          // compact mode: the alpha channel's update, dense [B,H,W] (K2 reads it over
+  float* dxa;          // compact mode: the alpha channel's update, [B,H,W], live cells only (K2 reads it over
                        // its band's halo rows without the row tables)
   uint64_t seed;
   int64_t rng_step;
@@ -1320,7 +1320,7 @@ struct K2Args {
   // compact update field (K1Args::rmask): null = dense dx; else K1's tile geometry
   const uint64_t* rmask;
   const uint32_t* rpre;
-  const float* dxa;        // dense [B,H,W] alpha-channel update (K1Args::dxa)
+  const float* dxa;        // [B,H,W] alpha-channel update of the live cells (K1Args::dxa)
   int TH, TW, tiles_x;
 };
 
@@ -1365,7 +1365,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   // compact update field (K1's rollout mode): per (band row incl. halo, K1 tile column) the row's
   // live mask, live cells before it in its tile, and the tile; per column its (tile column, column
   // in tile).  dx of a cell = its packed value if live, else 0 (K1 multiplies dead cells by 0); the
-  // alpha channel's dx is the dense plane a.dxa (the halo rows need no tables).
+  // alpha channel's dx is the [B,H,W] plane a.dxa (live cells written; dead cells masked by the row tables).
   constexpr bool compact = COMPACT;
   const int NCELL = a.TH * a.TW, txn = a.tiles_x;
   uint64_t* tab_m = reinterpret_cast<uint64_t*>(smem + (size_t)(2 * a.band + 2) * W);
@@ -1453,14 +1453,21 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
     if (gn) d = (d - mu) * rs * g3 + b3;
     return xa + fast_tanh(d) * a.gain;   // as the backward's BA (the same gate bits)
   };
+  // compact field: K1 writes the alpha plane for live cells only; a dead cell's update is 0 (its
+  // row's live mask, already in LDS for the band rows and the halo rows)
+  auto live_at = [&](int e) {
+    const int r = e / W, j = e - (e / W) * W;
+    const uint32_t ci = colinfo[j];
+    return ((tab_m[r * txn + (int)(ci >> 16)] >> (ci & 0xffffu)) & 1ull) != 0;
+  };
 #pragma unroll
   for (int u = 0; u < NA; ++u) {
     const int e = tid + u * kThreads;
-    if (e < na) at[e] = alpha_at(ax[u], ad[u]);
+    if (e < na) at[e] = alpha_at(ax[u], (compact && !live_at(e)) ? 0.f : ad[u]);
   }
   for (int e = tid + NA * kThreads; e < na; e += kThreads) {
     const size_t p = 3 * HW + (size_t)h0 * W + e;
-    at[e] = alpha_at(xb[p], compact ? a.dxa[(size_t)b * HW + (p - 3 * HW)] : db[p]);
+    at[e] = alpha_at(xb[p], compact ? (live_at(e) ? a.dxa[(size_t)b * HW + (p - 3 * HW)] : 0.f) : db[p]);
   }
   __syncthreads();
   for (int e = tid; e < nb; e += kThreads) {
