@@ -115,9 +115,9 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   L.sp = o; o += 2 * L.sp_slot;           // sender plane (floats), two slots
   L.ab = o; o += ks_a16(RHW);             // the preparer's alive bytes over the region
   L.lst = o; o += 2 * L.lst_slot;         // live-cell list (u16 cell indices), two slots
-  L.cnt = o; o += 16;                     // live cells per slot; the group counter
+  L.cnt = o; o += 16;                     // live cells per slot; group counter; staging-reads-done counter
   L.cb = o; o += ks_a16(8 * (TH * TW / 64 + 2));   // the preparer's 64-cell chunk ballots
-  L.pg = o; o += 16 * ((TH * TW + 31) / 32);     // per-group GroupNorm partials (fp64 pairs)
+  L.pg = o; o += 2 * 16 * ((TH * TW + 31) / 32);  // per-group GroupNorm partials (fp64 pairs), two slots
   L.w1 = o; o += 3 * 4 * 3 * 1024;       // [plane][rb][kc][lane] x 16 B
   L.bias = o; o += 4 * 32 * 16;          // [rb][row] x 16 B (k slots 0..2 = the three parts)
   L.w2 = o; o += 3 * 8 * 2 * 16 * 16;    // [plane][s][h][channel] x 16 B
@@ -126,23 +126,6 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   L.bml = o; o += 2 * 8 * 4;             // message bias per (lane half h, accumulator register r)
   L.total = o;
   return L;
-}
-
-// The next group of a tile: one LDS add by the whole wave (the counter moves by 64 per pull, so
-// the old value >> 6 is the group).  Inline asm: the compiler would otherwise treat the atomic as
-// possibly aliasing the in-flight LDS-DMA staging and wait for every outstanding memory operation
-// (the previous group's dx stores) first; the counter is never a DMA destination.
-#ifndef GNCA_K1_PULL
-#define GNCA_K1_PULL 1   // A/B builds only: 0 static (q = wave, wave + 8, ...), 2 inline-asm add (measured B=1024: 0.515, 0.460 (1), 0.470 ms)
-#endif
-__device__ __forceinline__ int pull_group(int* ctr) {
-  int old;
-  const int one = 1;
-  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
-               : "=v"(old)
-               : "v"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)ctr), "v"(one)
-               : "memory");
-  return __builtin_amdgcn_readfirstlane(old) >> 6;
 }
 
 template <int TH, int TW, int RY, int RX, int KU>
@@ -167,8 +150,13 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
 
   float* xs = reinterpret_cast<float*>(smem_b + L.xs);
   int* cnt = reinterpret_cast<int*>(smem_b + L.cnt);
-  int* gctr = cnt + 2;   // next group of the tile (LDS atomic)
-  double* pg = reinterpret_cast<double*>(smem_b + L.pg);
+  // LDS counters, monotonic over the workgroup's tiles (no resets: every wave's last pull of a tile
+  // fails exactly once, so the group counter advances by groups + NW per tile): gctr hands out
+  // groups (64 per pull, one per lane), xsd counts groups past their staged-plane reads (64 each)
+  int* gctr = cnt + 2;
+  int* xsd = cnt + 3;
+  int gbase = 0, xbase = 0;
+  constexpr int NG = (TH * TW + 31) / 32;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31, c16 = lane & 15;
@@ -260,13 +248,13 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
 
   // LDS-DMA staging of a tile's channel planes: 16-byte quads of every plane (torus-wrapped), lanes
   // past the region masked off (the plane pads stay zero)
-  auto issue_dma = [&](int t) {
+  auto issue_dma = [&](int t, int w0, int wstep) {
     const int b = t / a.tps, tin = t - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
     const float* xb = a.x + (size_t)b * C * HW;
 #pragma unroll 1
-    for (int ii_ = wave; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI4); ii_ += NW) {
+    for (int ii_ = w0; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI4); ii_ += wstep) {
       const int q = 64 * ii_ + lane;
       if (q < NQ) {
         const int e = 4 * q, vr = e / RW, vc = e - (e / RW) * RW;
@@ -377,9 +365,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
 
   PROF_DECL
   int tile = next_active(t_begin + xr_);
-  if (tile < t_end) issue_dma(tile);
+  if (tile < t_end) issue_dma(tile, wave, NW);
   if (wave == PW && tile < t_end) prep(tile, 0);
-  if (tid == 0) *gctr = 0;
+  if (tid == 0) { *gctr = 0; *xsd = 0; }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch; the
   // other case reads the weights from global memory, an uncommon slow path)
@@ -426,24 +414,20 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
     const uint16_t* lst = reinterpret_cast<const uint16_t*>(smem_b + L.lst + par * L.lst_slot);
     const int nlive = cnt[par];
 
-    if (wave == PW && nxt < t_end) prep(nxt, par ^ 1);
+    if (wave == PW && nxt < t_end && !(GNCA_ABLATE & kAblPrep)) prep(nxt, par ^ 1);
     PROF_MARK(3);   // preparer
 
     // ---- 32-cell groups, pulled from an LDS counter (the faster, older wave of a SIMD takes more);
     //      each group's GroupNorm partials go to pg[q], so the sums do not depend on which wave ran it ----
     const int qend = (nlive + 31) >> 5;
+    double* pg = reinterpret_cast<double*>(smem_b + L.pg) + par * 2 * NG;
+    auto pull = [&]() { return (__builtin_amdgcn_readfirstlane(atomicAdd(gctr, 1)) >> 6) - gbase; };
     const bool img_top = i0 == 0, img_bot = i0 + TH == H, img_lft = j0 == 0, img_rgt = j0 + TW == W;
-#pragma unroll 1
     // (every lane adds 1: the wave's 64 increments are one LDS instruction, so the counter moves by
     //  64 per pull and any lane's old value >> 6 is the pulled group)
-#if GNCA_K1_PULL == 0
-    for (int q = wave; q < qend; q += NW) {
-#elif GNCA_K1_PULL == 1
-    for (int q = __builtin_amdgcn_readfirstlane(atomicAdd(gctr, 1)) >> 6; q < qend;
-         q = __builtin_amdgcn_readfirstlane(atomicAdd(gctr, 1)) >> 6) {
-#else
-    for (int q = pull_group(gctr); q < qend; q = pull_group(gctr)) {
-#endif
+    int q = pull();
+#pragma unroll 1
+    for (; q < qend; q = pull()) {
       float s1 = 0.f, s2 = 0.f;
       const int gi = 32 * q + r32;
       const bool valid = gi < nlive;
@@ -539,6 +523,8 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       split3_x8(y0, yf[0][0], yf[0][1], yf[0][2]);
       split3_x8(y1, yf[1][0], yf[1][1], yf[1][2]);
       split3_x8(y2, yf[2][0], yf[2][1], yf[2][2]);
+      // this group's reads of the staged planes are done (release: they stay before the count)
+      __hip_atomic_fetch_add(xsd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (GNCA_ABLATE & kAblMfma) {
 #pragma unroll
         for (int kc = 0; kc < 3; ++kc) asm volatile("" ::"v"(yf[kc][0]), "v"(yf[kc][1]), "v"(yf[kc][2]));
@@ -640,9 +626,20 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
     }
 
     PROF_MARK(4);   // group loop
-    __syncthreads();   // this tile's groups are done (staged planes free, pg complete, slot par^1 ready)
+    // The wave whose pull failed first (q == qend: the counter hands out consecutive values) stages
+    // the next tile as soon as every group is past its staged-plane reads, while the other waves
+    // still run their last groups' MFMAs and stores.
+    if (q == qend && nxt < t_end) {
+      while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xbase < qend)
+        __builtin_amdgcn_s_sleep(1);
+      issue_dma(nxt, 0, 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    PROF_MARK(0);
+    __syncthreads();   // groups done, next tile staged, pg complete, slot par^1 ready
     PROF_MARK(6);
-    if (tid == 0) *gctr = 0;
+    gbase += qend + NW;
+    xbase += qend;
     // ---- the tile's GroupNorm partials in 8 bins (bin j: groups j, j + 8, ... in order; K2 sums the
     //      bins of a sample in fixed order) ----
     if (tid < 2 * NW) {
@@ -651,13 +648,6 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
       a.stats[(size_t)tile * 2 * NW + tid] = s_;
     }
     PROF_MARK(5);   // per-tile reduction
-    if (nxt < t_end) {
-      issue_dma(nxt);
-      PROF_MARK(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      PROF_MARK(1);
-    }
     tile = nxt;
     par ^= 1;
   }

@@ -56,6 +56,7 @@ constexpr int kAblZero = 128;    // skip the dead-cell zero stores of the compac
 constexpr int kAblReduce = 256;  // skip the per-tile GroupNorm partial reduction
 constexpr int kAblTiles = 512;   // skip the tile loop (times launch + prologue)
 constexpr int kAblFill = 1024;   // skip the weight fill (LDS keeps old data)
+constexpr int kAblPrep = 2048;   // split K1: skip the preparer after the first tile (slots keep old lists)
 constexpr uint32_t kMsgOnly = 1u << 16;   // internal K1 flag: write agg message, skip MLP
 constexpr uint32_t kGraphOn = 1u << 17;   // internal K1 flag: gather + message projection needed
 

@@ -17,7 +17,7 @@ VARIANTS = {
     "no_planes": 32, "mfma_only": 1 | 2 | 4 | 16 | 32, "no_mfma_no_store": 8 | 16,
     "stage_only": 2 | 4 | 8 | 16 | 32,
     "no_fire": 64, "no_zero": 128, "no_reduce": 256,
-    "no_tiles": 512, "no_tiles_no_fill": 512 | 1024, "lds_lite": 4096,
+    "no_prep": 2048, "no_prep_no_stage": 2049, "no_tiles": 512, "no_tiles_no_fill": 512 | 1024, "lds_lite": 4096,
     "bare": 2 | 4 | 8 | 16 | 32 | 64 | 128 | 256, "bare_no_stage": 1 | 2 | 4 | 8 | 16 | 32 | 64 | 128 | 256,
 }
 
@@ -115,8 +115,8 @@ def run(reps=15, rounds=3):
     full = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16).astype(np.float64)
     ws = full[:, 8:].sum() > 0
     if os.environ.get("ABLATE_PROF_SETS") == "w03":   # the split K1: wave 0 and the preparer wave 3
-        names = ["dma_issue", "dma_wait+barrier", "-", "preparer", "groups", "reduction",
-                 "barrier_before_dma", "loop_top"]
+        names = ["dma_issue", "dma_wait+barrier", "-", "preparer", "groups", "partial_bins",
+                 "barrier_after_groups", "loop_top"]
         sets = [("wave 0 (SIMD 0, older)", names, full[:, :8]),
                 ("wave 3 (SIMD 3, preparer)", names, full[:, 8:])]
     elif os.environ.get("ABLATE_PROF_SETS") == "w04":   # the split K1: both waves of SIMD 0
