@@ -5,10 +5,13 @@
 // fp32 MFMA issue (1/16 of the bf16 rate, on the VALU datapath).  Here every product is six exact
 // bf16 products (numerics as gnca_k1_split.h: fp32-class, dropped terms <= 2^-24 |a||b| each).
 //
-// Tile pipeline (as gnca_k1_2ph): 16x16 tiles, the region's channel planes staged in two
-// 16-channel phases through one LDS buffer (dword LDS-DMA: RW = 26 is not quad-aligned), alive /
-// sender / keep planes, live-cell compaction, one 32-cell group per wave (<= 8 groups per tile),
-// every accumulator of the group kept in registers across the phase boundary.
+// Tile pipeline: 16x16 tiles, the region's channel planes staged in two 16-channel phases through
+// one LDS buffer (dword LDS-DMA: RW = 26 is not quad-aligned), one 32-cell group per wave (<= 8
+// groups per tile), every accumulator of the group kept in registers across the phase boundary.
+// As in gnca_k1_split.h: a preparer wave (wave 7, which has no group unless > 224 cells of the tile
+// are live) builds the next tile's sender plane, keep mask, live-cell list and compact-field row
+// tables into a second LDS slot while the groups run, and stages the next tile's phase-0 planes
+// as soon as every group is past its phase-1 reads, under the groups' MFMAs.
 //
 // MFMA (v_mfma_f32_32x32x16_bf16; lane l: cell l & 31, half h = l >> 5; D reg r -> row
 // (r&3) + 8(r>>2) + 4h):
@@ -26,21 +29,23 @@
 namespace gnca {
 
 struct KS32Layout {
-  int xs, sp, al, kp, lst, wcnt, w1, bias, w2, wm, bml, total;   // byte offsets
+  int xs, sp, ab, lst, cnt, cb, w1, bias, w2, wm, bml, total;   // byte offsets
+  int sp_slot, lst_slot;                                         // bytes per prepared-tile slot
 };
 
 template <int TH, int TW, int RY, int RX>
 __host__ __device__ constexpr KS32Layout ks32_layout() {
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
-  constexpr int NI = (RHW + 63) / 64, NIA = ((RH + 2) * (RW + 2) + 63) / 64;
   KS32Layout L{};
   int o = 0;
+  L.sp_slot = ks_a16(RHW * 4);
+  L.lst_slot = ks_a16(TH * TW * 2);
   L.xs = o; o += 16 * ks_pstr(RHW) * 4;           // one phase's 16 channel planes
-  L.sp = o; o += ks_a16(RHW * 4);
-  L.al = o; o += 64 * 4 * (NIA > NI ? NIA : NI);  // alive bytes (one per dword) or the alpha ring
-  L.kp = o; o += ks_a16(TH * TW);
-  L.lst = o; o += ks_a16(TH * TW * 2);
-  L.wcnt = o; o += 32;
+  L.sp = o; o += 2 * L.sp_slot;                   // sender plane, two slots
+  L.ab = o; o += ks_a16(RHW);                     // the preparer's alive bytes over the region
+  L.lst = o; o += 2 * L.lst_slot;                 // live-cell list, two slots
+  L.cnt = o; o += 16;                             // live cells per slot; staged-reads-done counter
+  L.cb = o; o += ks_a16(8 * (TH * TW / 64 + 2));  // the preparer's 64-cell chunk ballots
   L.w1 = o; o += 4 * 3 * 2 * 3 * 1024;            // [rb][f][p][part][lane] x 16 B
   L.bias = o; o += 4 * 32 * 16;                   // [rb][row] x 16 B
   L.w2 = o; o += 8 * 3 * 1024;                    // [s][part][lane] x 16 B
@@ -57,7 +62,6 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
   constexpr int PSTR = ks_pstr(RHW);
   constexpr int NI = (RHW + 63) / 64;
-  constexpr int ALW = RW + 2, NIA = ((RH + 2) * ALW + 63) / 64;
   constexpr int NCELL = TH * TW;
   constexpr KS32Layout L = ks32_layout<TH, TW, RY, RX>();
   static_assert(NCELL <= 32 * NW, "one 32-cell group per wave");
@@ -65,13 +69,12 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   static_assert(L.total <= 160 * 1024, "LDS");
   static_assert(7 * PSTR * 4 + 4 * RHW < 65536, "channel offsets fit the DS immediate");
   constexpr bool GRAPH = KU > 0;
+  constexpr int PW = NW - 1;   // the preparer / next-tile stager (no group unless > 224 live cells)
 
   float* xs = reinterpret_cast<float*>(smem_b + L.xs);
-  float* sp = reinterpret_cast<float*>(smem_b + L.sp);
-  float* al = reinterpret_cast<float*>(smem_b + L.al);
-  uint8_t* kp = reinterpret_cast<uint8_t*>(smem_b + L.kp);
-  uint16_t* lst = reinterpret_cast<uint16_t*>(smem_b + L.lst);
-  int* wcnt = reinterpret_cast<int*>(smem_b + L.wcnt);
+  int* cnt = reinterpret_cast<int*>(smem_b + L.cnt);
+  int* xsd = cnt + 2;   // groups past their phase-1 reads, 64 per group (monotonic over the tiles)
+  int xbase = 0;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31;
@@ -80,8 +83,134 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   const bool compact = a.rmask != nullptr;   // the rollout's compact update field (gnca_k1_split.h)
   static_assert(TW <= 64, "one ballot per tile row (compact update field)");
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
-  const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
+  const size_t HW = (size_t)H * W;
 
+  // XCD-aware tile order (as gnca_k1_update)
+  const int nxcd = gridDim.x >= 8 ? 8 : 1;
+  const int xg_ = blockIdx.x % nxcd, xr_ = blockIdx.x / nxcd;
+  const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
+  const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
+  const int t_begin = xg_ * tq + min(xg_, trm), t_end = (GNCA_ABLATE & kAblTiles) ? t_begin : t_begin + tq + (xg_ < trm ? 1 : 0);
+  auto next_active = [&](int t) {
+    while (t < t_end && a.active && !a.active[t / a.tps]) {
+      if (tid < 2 * NW) a.stats[(size_t)t * 2 * NW + tid] = 0.0;
+      t += per_x;
+    }
+    return t;
+  };
+
+  // channel planes [16ph, 16ph + 16) of tile t's (RH x RW) region -> xs (torus-wrapped), dword DMA
+  // blocks w0, w0 + wstep, ...
+  auto stage = [&](int t, int ph, int w0, int wstep) {
+    const int b = t / a.tps, tin = t - b * a.tps;
+    const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+    const int i0 = ty * TH, j0 = tx * TW;
+    const float* xb = a.x + (size_t)b * C * HW;
+#pragma unroll 1
+    for (int ii_ = w0; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI); ii_ += wstep) {
+      const int e = 64 * ii_ + lane;
+      if (e < RHW) {   // lanes past the region masked off: the plane pads (zero taps) stay zero
+        const int vr = e / RW, vc = e - (e / RW) * RW;
+        int ii = i0 - RY + vr, jj = j0 - RX + vc;
+        ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
+        jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
+        const float* src0 = xb + (size_t)(16 * ph) * HW + ii * W + jj;
+        float* dst = xs + 64 * ii_;
+#pragma unroll 4
+        for (int c = 0; c < 16; ++c)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (size_t)c * HW),
+                                           (__attribute__((address_space(3))) void*)(dst + c * PSTR), 4, 0, 0);
+      }
+    }
+  };
+
+  // The preparer (one wave): tile t's sender plane over the region, keep = fire AND pre-alive, the
+  // live-cell list into slot s, the compact field's row tables (and, dense field, the dead cells'
+  // zeros).  The pre-update masks are the alive bytes (the previous K2's, or gnca_k_alive's).
+  auto prep = [&](int t, int s) {
+    const int b = t / a.tps, tin = t - b * a.tps;
+    const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+    const int i0 = ty * TH, j0 = tx * TW;
+    const size_t cell0 = (size_t)i0 * W + j0;
+    float* spp = reinterpret_cast<float*>(smem_b + L.sp + s * L.sp_slot);
+    uint16_t* lstp = reinterpret_cast<uint16_t*>(smem_b + L.lst + s * L.lst_slot);
+    uint8_t* abq = reinterpret_cast<uint8_t*>(smem_b + L.ab);
+    uint64_t* cb = reinterpret_cast<uint64_t*>(smem_b + L.cb);
+    {
+      const uint8_t* alb = a.alive + (size_t)b * HW;
+      constexpr int NU = (RHW + 63) / 64;
+      uint32_t v[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int e = 64 * u + lane;
+        v[u] = 0u;
+        if (e < RHW) {
+          const int vr = e / RW, vc = e - (e / RW) * RW;
+          int ii = i0 - RY + vr, jj = j0 - RX + vc;
+          ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
+          jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
+          v[u] = alb[ii * W + jj];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int e = 64 * u + lane;
+        if (e < RHW) {
+          abq[e] = (uint8_t)v[u];
+          if constexpr (GRAPH) spp[e] = a2a ? (float)((v[u] >> 1) & 1u) : 1.f;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float* outb = a.out + (size_t)b * C * HW + cell0;
+    int nl = 0;
+#pragma unroll 1
+    for (int n0 = 0; n0 < NCELL; n0 += 64) {
+      const int n = n0 + lane;
+      const bool inb = n < NCELL;
+      const int ti = n / TW, tj = n - (n / TW) * TW;
+      const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
+      bool live = false;
+      if (inb && (abq[(ti + RY) * RW + tj + RX] & 1u))
+        live = fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step, a.sample_base, b, HW, cell);
+      const uint64_t bal = __ballot(live);
+      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) cb[n0 >> 6] = bal;
+      if (compact && inb && tj == 0) a.rpre[(size_t)t * TH + ti] = (uint32_t)(nl + pre);
+      if (live) {
+        lstp[nl + pre] = (uint16_t)n;
+      } else if (inb && !compact) {   // (compact: K2 masks the alpha plane by the row tables)
+        float* oz = outb + (size_t)ti * W + tj;
+#pragma unroll
+        for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
+      }
+      nl += __popcll(bal);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (compact) {
+#pragma unroll 1
+      for (int ti = lane; ti < TH; ti += 64) {
+        const int f = ti * TW, c0 = f >> 6, sh = f & 63;
+        uint64_t m = cb[c0] >> sh;
+        if (sh + TW > 64) m |= cb[c0 + 1] << (64 - sh);
+        if (TW < 64) m &= (1ull << TW) - 1ull;
+        a.rmask[(size_t)t * TH + ti] = m;
+      }
+    }
+    if (lane == 0) cnt[s] = nl;
+  };
+
+  // prologue: the first tile's phase-0 DMA and planes, then the weight images
+  int tile = next_active(t_begin + xr_);
+  if (tile < t_end) stage(tile, 0, wave, NW);
+  if (wave == PW && tile < t_end) prep(tile, 0);
+  if (tid == 0) *xsd = 0;
+
+  // ---- weight images (bf16 parts in MFMA fragment order), once per persistent workgroup ----
   // ---- weight images (bf16 parts in MFMA fragment order), once per persistent workgroup ----
   {
     // W1: entry (rb, f, p, l): W1[32rb + (l&31)][32f + 16p + 8(l>>5) + 0..7]
@@ -144,6 +273,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     // the perception zero tap: every channel plane's pad floats (never written by the staging)
     for (int e = tid; e < 16 * (PSTR - RHW); e += NT) xs[(e / (PSTR - RHW)) * PSTR + RHW + e % (PSTR - RHW)] = 0.f;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int ok = 1;
   for (int idx = tid; idx < C * 27; idx += NT) {
     const int e = idx % 27, f = e / 9, tap = e % 9, tr = tap / 3, tc = tap % 3;
@@ -153,165 +283,24 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     else ref = (float)((tr == 0 ? 1 : (tr == 2 ? -1 : 0)) * (tc == 1 ? 2 : 1));
     if (a.perc[idx] != ref) ok = 0;
   }
-  const bool sobel = __syncthreads_and(ok) != 0;   // also the barrier after the image stores
+  const bool sobel = __syncthreads_and(ok) != 0;   // also the barrier after the images, DMA and prep
 
   const u32x4 ones = h == 0 ? u32x4{0x3f803f80u, 0x3f80u, 0u, 0u} : u32x4{0u, 0u, 0u, 0u};
   const float mgain = GRAPH ? a.message_gain : 0.f;
   const bool hz = hidden_only && h == 0;   // channels (r&3) + 4h < 4 (r < 4) are the RGBA ones
-  const size_t HW = (size_t)H * W;
 
-  // XCD-aware tile order (as gnca_k1_update)
-  const int nxcd = gridDim.x >= 8 ? 8 : 1;
-  const int xg_ = blockIdx.x % nxcd, xr_ = blockIdx.x / nxcd;
-  const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
-  const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
-  const int t_begin = xg_ * tq + min(xg_, trm), t_end = t_begin + tq + (xg_ < trm ? 1 : 0);
-  for (int tile = t_begin + xr_; tile < t_end; tile += per_x) {
+  int par = 0;
+  while (tile < t_end) {
+    const int nxt = next_active(tile + per_x);
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
-    const float* xb = a.x + (size_t)b * C * HW;
-    if (a.active && !a.active[b]) {   // inactive sample (masked step)
-      if (tid < 2 * NW) a.stats[(size_t)tile * 2 * NW + tid] = 0.0;
-      continue;
-    }
-    // channel planes [16ph, 16ph + 16) of the (RH x RW) region -> xs (torus-wrapped), dword DMA
-    auto stage = [&](int ph) {
-#pragma unroll 1
-      for (int ii_ = wave; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI); ii_ += NW) {
-        const int e = 64 * ii_ + lane;
-        if (e < RHW) {   // lanes past the region masked off: the plane pads (zero taps) stay zero
-          const int vr = e / RW, vc = e - (e / RW) * RW;
-          int ii = i0 - RY + vr, jj = j0 - RX + vc;
-          ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
-          jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-          const float* src0 = xb + (size_t)(16 * ph) * HW + ii * W + jj;
-          float* dst = xs + 64 * ii_;
-#pragma unroll 4
-          for (int c = 0; c < 16; ++c)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (size_t)c * HW),
-                                             (__attribute__((address_space(3))) void*)(dst + c * PSTR), 4, 0, 0);
-        }
-      }
-    };
-    __syncthreads();   // the previous tile's LDS readers are done
-    stage(0);
-    if (a.alive) {
-      // the previous K2's alive bytes over the region, one byte per dword
-      const uint8_t* ab = a.alive + (size_t)b * HW;
-#pragma unroll 1
-      for (int ii_ = wave; ii_ < NI; ii_ += NW) {
-        const int e = 64 * ii_ + lane;
-        int off = 0;
-        if (e < RHW) {
-          const int vr = e / RW, vc = e - (e / RW) * RW;
-          int ii = i0 - RY + vr, jj = j0 - RX + vc;
-          ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
-          jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-          off = ii * W + jj;
-        }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ab + off),
-                                         (__attribute__((address_space(3))) void*)(al + 64 * ii_), 1, 0, 0);
-      }
-    } else {
-      // alpha plane with one more ring: element e of ((RH+2) x ALW) -> (i0-RY-1+vr, j0-RX-1+vc)
-#pragma unroll 1
-      for (int ii_ = wave; ii_ < NIA; ii_ += NW) {
-        const int e = 64 * ii_ + lane;
-        int off = 0;
-        if (e < (RH + 2) * ALW) {
-          const int vr = e / ALW, vc = e - (e / ALW) * ALW;
-          int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
-          while (ii < 0) ii += H;
-          while (ii >= H) ii -= H;
-          while (jj < 0) jj += W;
-          while (jj >= W) jj -= W;
-          off = ii * W + jj;
-        }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xb + 3 * HW + off),
-                                         (__attribute__((address_space(3))) void*)(al + 64 * ii_), 4, 0, 0);
-      }
-    }
-    // ---- fire plane while the DMA is in flight ----
-#pragma unroll 1
-    for (int n = tid; n < NCELL; n += NT) {
-      const int ti = n / TW, tj = n - (n / TW) * TW;
-      const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
-      kp[n] = fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step, a.sample_base, b, HW, cell) ? 1 : 0;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    // ---- sender plane over the region, keep = pre-alive AND fire over the tile ----
-    if (a.alive) {
-      const int* alw = reinterpret_cast<const int*>(al);
-#pragma unroll 1
-      for (int pos = tid; pos < RHW; pos += NT) {
-        const int vr = pos / RW, vc = pos - (pos / RW) * RW;
-        const int v = alw[pos] & 0xff;
-        sp[pos] = a2a ? (float)((v >> 1) & 1) : 1.f;
-        const int ti = vr - RY, tj = vc - RX;
-        if (ti >= 0 && ti < TH && tj >= 0 && tj < TW && !(v & 1)) kp[ti * TW + tj] = 0;
-      }
-    } else {
-#pragma unroll 1
-      for (int pos = tid; pos < RHW; pos += NT) {
-        const int vr = pos / RW, vc = pos - (pos / RW) * RW;
-        int iq = i0 - RY + vr, jq = j0 - RX + vc;
-        while (iq < 0) iq += H;
-        while (iq >= H) iq -= H;
-        while (jq < 0) jq += W;
-        while (jq >= W) jq -= W;
-        const float* q = al + (vr + 1) * ALW + (vc + 1);
-        const float NEG = -INFINITY;
-        const bool up = iq > 0, dn = iq < H - 1, lf = jq > 0, rt = jq < W - 1;
-        const float mu_ = fmaxf(fmaxf(lf ? q[-ALW - 1] : NEG, q[-ALW]), rt ? q[-ALW + 1] : NEG);
-        const float mm_ = fmaxf(fmaxf(lf ? q[-1] : NEG, q[0]), rt ? q[1] : NEG);
-        const float md_ = fmaxf(fmaxf(lf ? q[ALW - 1] : NEG, q[ALW]), rt ? q[ALW + 1] : NEG);
-        const float mx = fmaxf(fmaxf(up ? mu_ : NEG, mm_), dn ? md_ : NEG);
-        sp[pos] = a2a ? (mx > gthr ? 1.f : 0.f) : 1.f;
-        const int ti = vr - RY, tj = vc - RX;
-        if (ti >= 0 && ti < TH && tj >= 0 && tj < TW && !(mx > thr)) kp[ti * TW + tj] = 0;
-      }
-    }
-    __syncthreads();
-
-    // ---- live-cell compaction (cell order, wave ballots: deterministic); dead cells get dx = 0 ----
     const size_t cell0 = (size_t)i0 * W + j0;
     float* outb = a.out + (size_t)b * C * HW + cell0;
-    int nlive = 0;
-    {
-      const int n = tid;
-      const bool inb = n < NCELL;
-      const bool live = inb && kp[n] != 0;
-      const uint64_t bal = __ballot(live);
-      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-      if (lane == 0) wcnt[wave] = __popcll(bal);
-      __syncthreads();
-      int off = 0;
-#pragma unroll
-      for (int w_ = 0; w_ < NW; ++w_) {
-        off += w_ < wave ? wcnt[w_] : 0;
-        nlive += wcnt[w_];
-      }
-      if (compact && inb && n % TW == 0) a.rpre[(size_t)tile * TH + n / TW] = (uint32_t)(off + pre);
-      if (live) {
-        lst[off + pre] = (uint16_t)n;
-      } else if (inb && !compact) {   // (compact: K2 masks the alpha plane by the row tables)
-        const int ti = n / TW, tj = n - (n / TW) * TW;
-        float* oz = outb + (size_t)ti * W + tj;
-#pragma unroll
-        for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
-      }
-      __syncthreads();
-    }
-    if (compact) {   // per-row live masks of the compact update field
-#pragma unroll 1
-      for (int ti_ = wave; ti_ < TH; ti_ += NW) {
-        const uint64_t m = __ballot(lane < TW && kp[ti_ * TW + (lane < TW ? lane : 0)] != 0);
-        if (lane == 0) a.rmask[(size_t)tile * TH + ti_] = m;
-      }
-    }
+    const float* sp = reinterpret_cast<const float*>(smem_b + L.sp + par * L.sp_slot);
+    const uint16_t* lst = reinterpret_cast<const uint16_t*>(smem_b + L.lst + par * L.lst_slot);
+    const int nlive = cnt[par];
+    if (wave == PW && nxt < t_end) prep(nxt, par ^ 1);
 
     // ---- one 32-cell group per wave; its accumulators live across the two channel phases ----
     const bool has = 32 * wave < nlive;   // wave-uniform
@@ -331,7 +320,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     for (int ph = 0; ph < 2; ++ph) {
       if (ph == 1) {
         __syncthreads();   // every wave is done with phase 0's planes
-        stage(1);
+        stage(tile, 1, wave, NW);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
       }
@@ -427,6 +416,18 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       __builtin_amdgcn_sched_barrier(0);
     }
 
+    // the next tile's phase-0 planes, staged by the preparer as soon as every group is past its
+    // phase-1 reads (release / acquire on the LDS counter), under the groups' MFMAs
+    const int ngrp = (nlive + 31) >> 5;
+    if (has) __hip_atomic_fetch_add(xsd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (wave == PW && nxt < t_end) {
+      while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xbase < ngrp)
+        __builtin_amdgcn_s_sleep(1);
+      stage(nxt, 0, 0, 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    xbase += ngrp;
+
     float s1 = 0.f, s2 = 0.f;
     if (has && !(GNCA_ABLATE & kAblMfma)) {
       // -- message: chunks p = 0, 1, 6 products each --
@@ -519,6 +520,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       a.stats[((size_t)tile * NW + wave) * 2 + 0] = d1;
       a.stats[((size_t)tile * NW + wave) * 2 + 1] = d2;
     }
+    __syncthreads();   // groups done; the next tile's phase 0 staged; slot par^1 ready
+    tile = nxt;
+    par ^= 1;
   }
 }
 

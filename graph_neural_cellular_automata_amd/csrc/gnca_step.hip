@@ -2194,9 +2194,9 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   fill_k1(k1, d, w, P, x, dx, fire, want_attn ? attn : nullptr, wsb);
   k1.active = active;
   uint8_t* alive = reinterpret_cast<uint8_t*>(wsb + P.off_alive);
-  // the 16-channel split K1 always reads the masks as bytes (its preparer wave builds the planes
-  // from them): without a hand-over from the previous K2, gnca_k_alive makes them first
-  const bool bytes_k1 = P.var->split == 1;
+  // the split K1s always read the masks as bytes (their preparer wave builds the planes from
+  // them): without a hand-over from the previous K2, gnca_k_alive makes them first
+  const bool bytes_k1 = P.var->split > 0;
   k1.alive = (alive_in || bytes_k1) ? alive : nullptr;
   if ((phases & GNCA_PHASE_K1) && bytes_k1 && !alive_in) {
     const size_t cells = (size_t)d->B * d->H * d->W;
