@@ -388,3 +388,38 @@ def test_c32_two_phase_path_vs_oracle(dev, msg):
         dt.rng_step = t
         cur, _ = S.step(dt, w, cur)
     assert torch.equal(r, cur)
+
+
+def test_masked_step_many_tiles_per_workgroup(dev):
+    """The 16-channel split K1 at B=256, 72^2: 1536 tiles of 24x36 over one persistent workgroup per
+    CU, so every workgroup walks several tiles and its preparer wave looks ahead past runs of
+    inactive samples (next_active).  The masked step's active samples equal the unmasked step's
+    bit for bit (samples are independent: per-sample GroupNorm, fire hashed by global sample
+    index); inactive samples pass through unchanged."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    m = _trained_like(dev, seed=3)
+    B, H = 256, 72
+    x = _state(B, 16, H, H, dev, seed=21)
+    random.seed(2)
+    offs = random.sample(m.graph.offsets, 8)
+    w, keep = S.make_weights(dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
+                                  b1=m.update_net[0].bias, w2=m.update_net[2].weight,
+                                  gn_weight=m.norm.weight, gn_bias=m.norm.bias,
+                                  **m.graph.weight_tensors()))
+    d = S.make_desc(B=B, C=16, H=H, W=H, hidden=128, d_model=16, offsets=offs,
+                    flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                    update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                    fire_mode=L.FIRE_HASH, rng_seed=7, rng_step=3, sample_base=0)
+    name = ctypes.create_string_buffer(64)
+    assert L.load().gnca_k1_variant(ctypes.byref(d), name, 64, None) == 0
+    assert name.value.decode().startswith("gnca_k1_split<24,36")
+    g = torch.Generator().manual_seed(4)
+    act = torch.rand(B, generator=g) < 0.5
+    act[10:40] = False                     # a long run of inactive samples
+    act[100:130] = True
+    act = act.to(dev)
+    full, _ = S.step(d, w, x)
+    masked, _ = S.step(d, w, x, active=act)
+    assert torch.equal(masked[act], full[act])
+    assert torch.equal(masked[~act], x[~act])
