@@ -128,6 +128,10 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   return L;
 }
 
+#ifndef GNCA_DMA_WAVES
+#define GNCA_DMA_WAVES 1   // A/B builds: waves (the first failing pulls) sharing the next tile's DMA (3: K1 0.4015-0.4044 vs 0.4008-0.4026 ms with 1)
+#endif
+
 template <int TH, int TW, int RY, int RX, int KU>
 __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_b[];
@@ -637,10 +641,10 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
     // The wave whose pull failed first (q == qend: the counter hands out consecutive values) stages
     // the next tile as soon as every group is past its staged-plane reads, while the other waves
     // still run their last groups' MFMAs and stores.
-    if (q == qend && nxt < t_end) {
+    if (q >= qend && q < qend + GNCA_DMA_WAVES && nxt < t_end) {
       while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xbase < qend)
         __builtin_amdgcn_s_sleep(1);
-      issue_dma(nxt, 0, 1);
+      issue_dma(nxt, q - qend, GNCA_DMA_WAVES);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     PROF_MARK(0);
