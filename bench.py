@@ -10,8 +10,10 @@ counter RNG keyed by global sample index, so the N-GPU run computes exactly the 
 1-GPU run would for the same samples.  ``--config c2|c3|c5`` runs the other BASELINE.json GPU
 configs (classic B=8; graph B=8; 32ch 128^2 r=5 K=16) with the same harness.
 
-Multi-GPU: one process per GPU (torchrun), B samples per rank (weak scaling), no collective on
-the data path; barrier + synchronize around the timed region, max time over ranks.
+Multi-GPU: one process per GPU, B samples per rank (weak scaling), no collective on the data path;
+barrier + synchronize around the timed region, max time over ranks.  Launched either by
+``torch.distributed.run --nproc-per-node N bench.py --gpus N`` or as plain ``bench.py --gpus N``,
+which starts the N ranks itself (torch.distributed.run on 127.0.0.1) before touching the GPU.
 
 Prints ONE JSON line on rank 0.
 """
@@ -24,6 +26,8 @@ import json
 import os
 import platform
 import random
+import socket
+import subprocess
 import sys
 import time
 
@@ -70,9 +74,21 @@ def flop_per_cell(wl):
 
 def pmc_traffic(kernel):
     try:
-        import json as _j
-        d = _j.load(open(PMC_TRAFFIC))["kernels"][kernel]
+        d = json.load(open(PMC_TRAFFIC))["kernels"][kernel]
         return d["traffic_bytes"]
+    except Exception:
+        return None
+
+
+def pmc_mfma_busy(kernel, cus):
+    """MFMA pipe busy fraction of ``kernel`` from the committed PMC pass (profiles/*_pmc_traffic.json):
+    SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over every SIMD: 32 per v_mfma_f32_32x32x16_bf16) /
+    (GRBM_GUI_ACTIVE / 8 XCDs = the kernel's cycles, x 4 SIMDs x CUs)."""
+    try:
+        c = json.load(open(PMC_TRAFFIC))["kernels"][kernel]["counters"]
+        busy, grbm = c["SQ_VALU_MFMA_BUSY_CYCLES"], c["GRBM_GUI_ACTIVE"]
+        return {"value": busy / (grbm / 8 * 4 * cus), "source": os.path.relpath(PMC_TRAFFIC, ROOT),
+                "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 4 SIMDs x CUs)"}
     except Exception:
         return None
 
@@ -90,8 +106,8 @@ def parse():
                     help="rollout workload (BASELINE.json configs); default: the roofline headline")
     ap.add_argument("--batch", type=int, default=None, help="samples per GPU (default: the config's)")
     ap.add_argument("--size", type=int, default=None, help="canvas (default: the config's)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="wall budget of the CPU-baseline sample (rank 0, N=1 only)")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0,
+                    help="wall budget of the CPU baseline (rank 0, N=1 only), split over its entries")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) on a node; gloo only to rehearse N>1 ranks on one GPU")
@@ -131,40 +147,18 @@ def make_desc(wl, B, H, W, offsets, rank, step0=0):
                        fire_mode=L.FIRE_HASH, rng_seed=42, rng_step=step0, sample_base=rank * B)
 
 
-def cpu_baseline(budget_s: float, wl, H: int):
-    """The numpy oracle (float32, the reference's arithmetic) on host cores: a B<=8 sample of the
-    same workload, stepped until the wall budget is spent (>= 2 steps)."""
-    from oracle import nca_oracle as O
+def _host_cores():
+    """(threads to use for "all cores", description): the CPUs this process may run on (affinity),
+    capped by a cgroup CPU quota when one is set (a GPU box's share of a larger host)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
     try:
-        from threadpoolctl import threadpool_limits
-    except Exception:  # pragma: no cover
-        threadpool_limits = None
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(16, ncpu))
-    z = np.load(os.path.join(GOLDEN, wl["fixture"] + ".npz"), allow_pickle=False)
-    p = {k[2:]: z[k].astype(np.float32) for k in z.files if k.startswith("w:")}
-    cfg = dict(update_gain=GAIN, alpha_thr=THR, use_groupnorm=True, graph=wl["graph"],
-               message_gain=MSG_GAIN, hidden_only=True, zero_padded_shift=False, alive_to_alive=True)
-    C = wl["C"]
-    rng = np.random.default_rng(0)
-    B = min(8, wl["B"])
-    x = rng.random((B, C, H, H), dtype=np.float32)
-    x[:, 4:] = rng.standard_normal((B, C - 4, H, H), dtype=np.float32)
-    offs = O.build_offsets(wl["R"]) if wl["graph"] else []
-    rr = random.Random(42)
-    ctx = threadpool_limits(limits=threads) if threadpool_limits else None
-    steps = 0
-    t0 = time.perf_counter()
-    while True:
-        chosen = rr.sample(offs, wl["K"]) if wl["graph"] else None
-        fm = O.hash_fire_mask(42, steps, 0, B, H, H, FIRE)
-        x = O.nca_step(x, p, cfg, chosen=chosen, fire_mask=fm)
-        steps += 1
-        el = time.perf_counter() - t0
-        if steps >= 2 and el >= budget_s:
-            break
-    if ctx is not None:
-        ctx.__exit__(None, None, None)
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(float(q) / float(per) + 0.5))
+    except (OSError, ValueError):
+        pass
+    n = min(aff, quota) if quota else aff
     cpu = platform.processor() or platform.machine()
     try:
         for line in open("/proc/cpuinfo"):
@@ -173,12 +167,77 @@ def cpu_baseline(budget_s: float, wl, H: int):
                 break
     except OSError:
         pass
-    kind = f"graph torus r={wl['R']} K={wl['K']}" if wl["graph"] else "classic"
-    return {"value": B * H * H * steps / el, "unit": "cell-updates/s", "cores": threads,
-            "kind": "port",
-            "sample": f"numpy float32 oracle (oracle/nca_oracle.py), {kind} C{C} {H}x{H}, "
-                      f"B={B}, {steps} steps in {el:.1f}s; BLAS threads={threads}, elementwise "
-                      f"single-threaded; host CPU: {cpu}"}
+    return n, f"{cpu}; affinity {aff} CPUs" + (f", cgroup quota {quota} CPUs" if quota else "")
+
+
+# BASELINE.md CPU-baseline plan: configs C1-C4 (BASELINE.json configs[0..3]) on the PyTorch-CPU
+# restatement of the reference's op sequence, all cores and 1 thread.  Per entry: (graph, B, canvas,
+# steps of the config, B of the 1-thread sample) — C4's 1-thread leg times a B=64 slice of the pool
+# (one B=1024 step would take ~30 s on one core; the cost per cell does not depend on B there).
+CPU_CONFIGS = {
+    "C1": dict(graph=False, B=1, H=72, steps=64, B1=1,
+               name="classic NCA, B=1, 72^2, 64-step rollout (BASELINE config 1)"),
+    "C2": dict(graph=False, B=8, H=72, steps=96, B1=8, name="classic NCA, B=8, 72^2, 96 steps"),
+    "C3": dict(graph=True, B=8, H=72, steps=96, B1=8, name="graph NCA torus r=4 K=8, B=8, 72^2, 96 steps"),
+    "C4": dict(graph=True, B=1024, H=72, steps=96, B1=64,
+               name="graph NCA torus r=4 K=8, pool B=1024, 72^2 (the per-GPU headline shape)"),
+}
+
+
+def cpu_baseline(budget_s: float):
+    """The reference's CPU path restated in PyTorch (oracle/torch_cpu_ref.py, pinned by the golden
+    fixtures: reference op sequence, fp32, torch.rand fire mask) timed on this host for BASELINE
+    configs C1-C4 on all cores and on 1 thread.  Each entry steps the config's rollout until its
+    share of ``budget_s`` is spent (at least one step).  ``value`` is C4 on all cores (the workload
+    the GPU line measures)."""
+    from oracle.torch_cpu_ref import TorchCpuStep, build_offsets
+    threads, host = _host_cores()
+    gz = np.load(os.path.join(GOLDEN, WORKLOADS["headline"]["fixture"] + ".npz"), allow_pickle=False)
+    cz = np.load(os.path.join(GOLDEN, WORKLOADS["c2"]["fixture"] + ".npz"), allow_pickle=False)
+    steppers = {
+        True: TorchCpuStep({k[2:]: gz[k] for k in gz.files if k.startswith("w:")}, graph=True,
+                           update_gain=GAIN, alpha_thr=THR, message_gain=MSG_GAIN),
+        False: TorchCpuStep({k[2:]: cz[k] for k in cz.files if k.startswith("w:")}, graph=False,
+                            update_gain=GAIN, alpha_thr=THR),
+    }
+    offs = build_offsets(4)
+    old_threads = torch.get_num_threads()
+    entries = {}
+    per = budget_s / (2 * len(CPU_CONFIGS))
+    try:
+        for nthr in (threads, 1):
+            torch.set_num_threads(nthr)
+            for gr_ in (True, False):   # untimed: thread-pool start, first-call kernel setup
+                xw = torch.rand(2, 16, 72, 72)
+                steppers[gr_](xw, FIRE, random.Random(0).sample(offs, 8) if gr_ else None)
+            for name, c in CPU_CONFIGS.items():
+                B = c["B"] if nthr == threads else c["B1"]
+                g = torch.Generator().manual_seed(0)
+                x = torch.rand(B, 16, c["H"], c["H"], generator=g)
+                x[:, 4:] = torch.randn(B, 12, c["H"], c["H"], generator=g)
+                rr = random.Random(42)
+                st = steppers[c["graph"]]
+                n = 0
+                t0 = time.perf_counter()
+                while n < c["steps"]:
+                    x = st(x, FIRE, rr.sample(offs, 8) if c["graph"] else None)
+                    n += 1
+                    if time.perf_counter() - t0 >= per:
+                        break
+                el = time.perf_counter() - t0
+                entries[f"{name}_{'all' if nthr == threads else '1t'}"] = {
+                    "value": B * c["H"] * c["H"] * n / el, "threads": nthr, "batch": B, "steps": n,
+                    "seconds": round(el, 3), "workload": c["name"]}
+    finally:
+        torch.set_num_threads(old_threads)
+    head = entries["C4_all"]
+    return {"value": head["value"], "unit": "cell-updates/s", "cores": threads, "kind": "port",
+            "sample": f"PyTorch-CPU restatement of the reference step (oracle/torch_cpu_ref.py, fixture-"
+                      f"pinned; fp32, torch.rand fire mask 0.5, trained nca_latest.pt / nca_epoch980.pt "
+                      f"weights); value = C4 (graph B=1024 72^2 r=4 K=8) on {threads} threads, "
+                      f"{head['steps']} step(s) in {head['seconds']} s; entries: BASELINE configs C1-C4 "
+                      f"on all {threads} threads and on 1 thread (C4 1-thread: a B=64 slice); host: {host}",
+            "configs": entries}
 
 
 # The trainer configs (reference configs/config.json "training"/"damage" blocks): the graph
@@ -366,11 +425,30 @@ def main_train(args, dev, world, rank):
         dist.destroy_process_group()
 
 
+def launch_ranks(args) -> int:
+    """``--gpus N`` without a launcher: start N ranks (one process per GPU) under
+    torch.distributed.run on 127.0.0.1 and wait for them.  Runs BEFORE any GPU call in this
+    process (the parent never touches the GPU and never execs); returns the launcher's exit code."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: {world} ranks launched but --gpus {args.gpus}")
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(1, ndev))
     torch.cuda.set_device(dev)
@@ -380,6 +458,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus
     if args.mode == "train":
         return main_train(args, dev, world, rank)
     from graph_neural_cellular_automata_amd import _lib as L
@@ -394,6 +473,8 @@ def main():
     H = args.size or wl["H"]
     offsets_table = build_offsets(R) if graph else []
     w, w_keep = weight_struct(load_weights(dev, wl), wl)   # w_keep owns the tensors w points at
+    # this rank's samples are global samples [rank*B, (rank+1)*B): their start state and fire masks
+    # depend on the global index only, so rank 0 of an N-rank run computes the 1-rank run's states
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(B, C, H, H, device=dev, generator=g)
     x[:, 4:] = torch.randn(B, C - 4, H, H, device=dev, generator=g)
@@ -451,54 +532,61 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    cpu_dev = dev if args.dist_backend == "nccl" else "cpu"
+    ranks_seen = 1
+    rank_sums = [float(out.double().sum())]
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64,
-                         device=dev if args.dist_backend == "nccl" else "cpu")
+        t = torch.tensor([el], dtype=torch.float64, device=cpu_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+        one = torch.ones(1, dtype=torch.float64, device=cpu_dev)
+        dist.all_reduce(one)
+        ranks_seen = int(one.item())
+        sums = [torch.zeros(1, dtype=torch.float64, device=cpu_dev) for _ in range(world)]
+        dist.all_gather(sums, torch.tensor(rank_sums, dtype=torch.float64, device=cpu_dev))
+        rank_sums = [float(v.item()) for v in sums]
     cells = B * H * H
     value = cells * args.steps * world / el
 
-    # --- per-kernel average durations over the timed rollout: replay it launch by launch (same
-    #     start state, offsets and fire counters, so the same work; the final state is checked
-    #     bitwise against the timed rollout's) with HIP events around every K1 and K2 launch on
-    #     the launch stream.  Step 0's K1 computes the alive masks from alpha, later K1s read the
-    #     bytes the previous K2 wrote (PHASE_ALIVE), exactly as gnca_rollout_f32 runs them. ---
+    # --- what K1 executes per launch: replay the timed rollout launch by launch (same start state,
+    #     offsets and fire counters; the final state is checked bitwise against the timed one) and
+    #     count each launch's live cells (keep = pre-alive AND fire: K1 runs the MLP only for them,
+    #     the others have dx = 0 exactly) and, for the split K1, its padded 32-cell groups per tile.
+    #     Step 0's K1 reads alive bytes from gnca_k_alive, later K1s the previous K2's, exactly as
+    #     gnca_rollout_f32 runs them. ---
     d = make_desc(wl, B, H, H, offsets_table[:K], rank, args.warmup)
     k1_name, arith = S.k1_variant(d)
+    compact = S.rollout_compact(d)
     tile = None
     if arith == "bf16x6":
         th, tw, _, _, ku = [int(v) for v in k1_name.split("<")[1].rstrip(">").split(",")]   # <TH,TW,RY,RX,KU>
         tile = (th, tw)
-    bufs = [scratch, torch.empty_like(x)]
-    src = start
-    evs = []
-    live = torch.zeros((), dtype=torch.float64, device=dev)
-    groups = torch.zeros((), dtype=torch.int64, device=dev)
+    descs = []
     for t in range(args.steps):
         o = timed_offsets[2 * K * t: 2 * K * (t + 1)]
-        d = make_desc(wl, B, H, H, [(o[2 * j], o[2 * j + 1]) for j in range(K)] if graph else [],
-                      rank, args.warmup + t)
-        dst = bufs[t % 2]
-        # this launch's live cells (keep = pre-alive AND fire: K1 runs the MLP only for them, the
-        # others have dx = 0 exactly) and, for the split K1, its padded 32-cell groups per tile
-        kp = ((torch.nn.functional.max_pool2d(src[:, 3:4], 3, 1, 1) > THR) & (S.fire_mask(d, dev) != 0))[:, 0]
+        descs.append(make_desc(wl, B, H, H, [(o[2 * j], o[2 * j + 1]) for j in range(K)] if graph else [],
+                               rank, args.warmup + t))
+    bufs = [scratch, torch.empty_like(x)]
+    ph = L.PHASE_COMPACT if compact else 0
+
+    def launch(t, src, dst, which):
+        f = (L.PHASE_K1 | (L.PHASE_ALIVE if t > 0 else 0)) if which == 1 else (L.PHASE_K2 | L.PHASE_ALIVE)
+        L.check(lib.gnca_step_phases_f32(ctypes.byref(descs[t]), ctypes.byref(w), src.data_ptr(),
+                                         dst.data_ptr(), None, None, ws.data_ptr(), ws.numel(), sptr,
+                                         f | ph), f"k{which}")
+
+    live = torch.zeros((), dtype=torch.float64, device=dev)
+    groups = torch.zeros((), dtype=torch.int64, device=dev)
+    src = start
+    for t in range(args.steps):
+        kp = ((torch.nn.functional.max_pool2d(src[:, 3:4], 3, 1, 1) > THR) & (S.fire_mask(descs[t], dev) != 0))[:, 0]
         live += kp.sum()
         if tile:
             per_tile = kp.reshape(B, H // tile[0], tile[0], H // tile[1], tile[1]).sum(dim=(2, 4))
             groups += ((per_tile + 31) // 32).sum()
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        e[0].record(stream)
-        L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), src.data_ptr(), dst.data_ptr(),
-                                         None, None, ws.data_ptr(), ws.numel(), sptr,
-                                         L.PHASE_K1 | L.PHASE_COMPACT | (L.PHASE_ALIVE if t > 0 else 0)), "k1")
-        e[1].record(stream)
-        e[2].record(stream)
-        L.check(lib.gnca_step_phases_f32(ctypes.byref(d), ctypes.byref(w), src.data_ptr(), dst.data_ptr(),
-                                         None, None, ws.data_ptr(), ws.numel(), sptr,
-                                         L.PHASE_K2 | L.PHASE_COMPACT | L.PHASE_ALIVE), "k2")
-        e[3].record(stream)
-        evs.append(e)
+        dst = bufs[t % 2]
+        launch(t, src, dst, 1)
+        launch(t, src, dst, 2)
         src = dst
     torch.cuda.synchronize()
     if not torch.equal(src.view(torch.int32), out.view(torch.int32)):
@@ -506,21 +594,38 @@ def main():
         raise SystemExit(f"bench: the launch-by-launch replay differs from the timed rollout: "
                          f"{int(diff.sum())} values, max |d| {float((src - out).abs().nan_to_num().max()):.3e}, "
                          f"NaN {int(src.isnan().sum())}/{int(out.isnan().sum())}")
-    k1_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)
-    k2_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / len(evs)
+    # --- per-kernel durations: a second replay with ONLY the K1/K2 launches on the stream and a
+    #     HIP event between consecutive launches (no torch kernels in between) ---
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps + 1)]
+    src = start
+    torch.cuda.synchronize()
+    evs[0].record(stream)
+    for t in range(args.steps):
+        dst = bufs[t % 2]
+        launch(t, src, dst, 1)
+        evs[2 * t + 1].record(stream)
+        launch(t, src, dst, 2)
+        evs[2 * t + 2].record(stream)
+        src = dst
+    torch.cuda.synchronize()
+    if not torch.equal(src.view(torch.int32), out.view(torch.int32)):
+        raise SystemExit("bench: the timing replay differs from the timed rollout")
+    k1_all = [evs[2 * t].elapsed_time(evs[2 * t + 1]) for t in range(args.steps)]
+    k2_all = [evs[2 * t + 1].elapsed_time(evs[2 * t + 2]) for t in range(args.steps)]
+    k1_ms = sum(k1_all) / len(k1_all)
+    k2_ms = sum(k2_all) / len(k2_all)
     launches = args.steps
     live_frac = float(live) / (cells * launches)
     fpc = flop_per_cell(wl)
-    k1_flops = cells * fpc
-    compact = S.rollout_compact(d)
+    dense_flops = cells * fpc
+    live_flops = float(live) / launches * fpc
     # read x, write x'; read dx: dense NCHW, or on the compact field the alpha channel's dense
     # plane and the other channels' live values only
     k2_bytes = cells * 4 * (2 * C + (1 + (C - 1) * live_frac if compact else C))
     headline = args.config == "headline"
     # executed MFMA work per launch: live cells are packed into groups of 32 per tile (split K1,
     # v_mfma_f32_32x32x16_bf16 of 32,768 FLOP each per group: 16 channels 108 + 4 for the message,
-    # 32 channels 196 + 12; a tile's last group is padded) or, for the f32 K1, the dense FLOPs per
-    # live cell
+    # 32 channels 196 + 12; a tile's last group is padded) or, for the f32 K1, the FLOPs per live cell
     if arith == "bf16x6":
         per_group = (112 if ku else 108) if C == 16 else (208 if ku else 196)
         exec_flops = float(groups) / launches * per_group * 32768
@@ -528,29 +633,33 @@ def main():
         basis = ("bf16 MFMA dense peak (2.5 PFLOP/s) / 6: K1 runs every fp32 product as 6 exact "
                  "bf16 split products (gnca_k1_split.h)")
     else:
-        exec_flops = float(live) / launches * fpc
+        exec_flops = live_flops
         peak_dtype = peak_eq = PEAK_F32_MFMA
         basis = "fp32 MFMA peak (v_mfma_f32_*_f32)"
     k1_s = k1_ms * 1e-3
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    pmc_busy = pmc_mfma_busy("K1", cus) if headline else None
     roof = {"bound": "mfma", "kernel": k1_name, "arith": arith,
-            "achieved": k1_flops / k1_s / 1e12,
+            "achieved": live_flops / k1_s / 1e12,
             "peak": peak_eq / 1e12, "unit": "TFLOP/s",
-            "frac": k1_flops / k1_s / peak_eq,
+            "frac": live_flops / k1_s / peak_eq,
+            "flop_basis": f"executed fp32-equivalent FLOPs: the launch's live cells (keep = fire AND "
+                          f"pre-alive, {live_frac:.3f} of all cells; the others have dx = 0 exactly and "
+                          f"K1 skips their MLP) x {fpc:,} FLOP (SURVEY.md 8d) / K1's average duration",
             "peak_basis": basis,
-            "vs_f32_mfma_peak": k1_flops / k1_s / PEAK_F32_MFMA,
+            "dense_equiv_frac": dense_flops / k1_s / peak_eq,
+            "dense_flop_per_launch": dense_flops, "live_flop_per_launch": live_flops,
+            "live_fraction": live_frac,
             "traffic": pmc_traffic("K1") if headline else None,
             "traffic_unit": f"bytes/launch (2*FETCH_SIZE+WRITE_SIZE, {os.path.relpath(PMC_TRAFFIC, ROOT)})",
-            "k1_ms": k1_ms, "flop_per_launch": k1_flops,
-            "live_fraction": live_frac,
-            "executed_mfma_tflops": exec_flops / k1_s / 1e12,
-            "mfma_busy_frac": exec_flops / k1_s / peak_dtype,
-            "k1_launches_timed": launches,
-            "note": f"achieved = dense algorithmic fp32 FLOPs ({fpc:,} per cell-update, SURVEY.md 8d) "
-                    "/ K1's average duration over the timed rollout's launches (HIP events on the "
-                    "launch stream, launch-by-launch replay).  K1 runs the MLP only for live "
-                    "cells (keep = alive AND fire; the others have dx = 0 exactly), so the MFMA "
-                    "pipe's own utilisation is mfma_busy_frac (executed MFMA FLOPs in the MFMA's "
-                    "dtype, padded groups included, / that dtype's dense peak)"}
+            "k1_ms": k1_ms,
+            "k1_ms_source": "HIP events on the launch stream between consecutive launches of a replay "
+                            "of the timed rollout holding only its K1/K2 launches",
+            "mfma_pipe_frac_est": exec_flops / k1_s / peak_dtype,
+            "mfma_pipe_note": "executed MFMA FLOPs in the MFMA's dtype (32-cell groups, padding "
+                              "included) / that dtype's dense peak",
+            "mfma_busy_pmc": pmc_busy,
+            "k1_launches_timed": launches}
     roof_k2 = {"bound": "hbm", "kernel": "gnca_k2_finalize", "update_field": "compact" if compact else "dense",
                "achieved": k2_bytes / (k2_ms * 1e-3) / 1e9,
                "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": k2_bytes / (k2_ms * 1e-3) / PEAK_HBM,
@@ -560,23 +669,27 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(args.cpu_seconds, wl, H)
+            cpu = cpu_baseline(args.cpu_seconds)
         metric = ("cell-updates/sec (B·H·W·steps) for 16ch 72×72 rollout at 1/2/4/8 MI355X" if C == 16
                   else f"cell-updates/sec (B·H·W·steps) for {C}ch {H}×{H} rollout")
         wdesc = ("trained nca_latest.pt" if wl["graph"] and C == 16 else
                  "trained classic nca_epoch980.pt" if not wl["graph"] else
                  "seeded random init (W2 ~ N(0,0.02))")
+        ms = el / args.steps * 1e3
         line = {
             "metric": metric,
             "value": value, "unit": "cell-updates/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "gpu_warmup": {"ms": args.gpu_warmup_ms, "steps": gw_steps},
-            "ms_per_step": el / args.steps * 1e3,
+            "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic state (RGB,alpha~U(0,1), hidden~N(0,1)); {wdesc} weights from the "
                     f"committed golden fixture",
             "config": {"workload": wl["name"], "config": args.config,
                        "channels": C, "hidden": HD, "height": H, "width": H,
                        "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}"},
+            "ranks_seen": ranks_seen, "backend": (args.dist_backend if world > 1 else None),
+            "rank_state_checksums": rank_sums,
+            "k1_k2_ms_vs_step": (k1_ms + k2_ms) / ms,
             "roofline": roof, "roofline_k2": roof_k2, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

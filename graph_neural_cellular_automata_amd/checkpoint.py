@@ -30,8 +30,10 @@ def _epoch_num(name: str) -> int:
 
 
 def save_checkpoint(ckpt_dir, tag, model, optimizer, scheduler, epoch, global_step, config=None,
-                    *, latest: bool = False) -> str:
-    """Write ``<ckpt_dir>/nca_<tag>.pt`` (and ``nca_latest.pt`` when ``latest``)."""
+                    *, latest: bool = False, pool=None) -> str:
+    """Write ``<ckpt_dir>/nca_<tag>.pt`` (and ``nca_latest.pt`` when ``latest``).  ``pool``: a
+    sharded ``SamplePool`` whose private slot-index stream is saved too (``pool_rng_state``), so a
+    resumed run continues its sequence (an extra key; the reference trainer ignores it)."""
     os.makedirs(ckpt_dir, exist_ok=True)
     payload = {
         "epoch": int(epoch),
@@ -42,6 +44,8 @@ def save_checkpoint(ckpt_dir, tag, model, optimizer, scheduler, epoch, global_st
         "param_count": count_parameters(model),
         "global_step": int(global_step),
     }
+    if pool is not None and pool.rng_state() is not None:
+        payload["pool_rng_state"] = pool.rng_state()
     path = os.path.join(ckpt_dir, f"nca_{tag}.pt")
     torch.save(payload, path)
     if latest:
@@ -72,10 +76,10 @@ def pick_resume(ckpt_dir):
     return best_path, best_payload
 
 
-def load_checkpoint(payload, model, optimizer=None, scheduler=None) -> int:
+def load_checkpoint(payload, model, optimizer=None, scheduler=None, pool=None) -> int:
     """Restore model (``strict=False``), optimizer and scheduler state as the trainer's resume
-    does (an incompatible optimizer/scheduler state is reported and skipped).  Returns the epoch
-    to start from."""
+    does (an incompatible optimizer/scheduler state is reported and skipped), and a sharded pool's
+    slot-index stream when the payload has one.  Returns the epoch to start from."""
     missing, unexpected = model.load_state_dict(payload["model_state"], strict=False)
     if missing:
         print(f"[resume] missing model keys: {missing}", flush=True)
@@ -91,4 +95,6 @@ def load_checkpoint(payload, model, optimizer=None, scheduler=None) -> int:
             scheduler.load_state_dict(payload["scheduler_state"])
         except Exception as e:
             print(f"[warn] scheduler state not compatible, reinit: {e}", flush=True)
+    if pool is not None and payload.get("pool_rng_state") is not None:
+        pool.set_rng_state(payload["pool_rng_state"])
     return int(payload.get("epoch", 0)) + 1

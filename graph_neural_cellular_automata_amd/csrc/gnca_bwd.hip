@@ -1520,7 +1520,7 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   // (padded cells + staged halo) within 160 KB of LDS
   static const int ths[] = {4, 8, 16};
   static const int tws[] = {8, 16, 24, 32};
-  static const char* tile_env = getenv("GNCA_BB_TILE");   // measurement knob (A/B runs only)
+  static const char* tile_env = GNCA_AB_ENV("GNCA_BB_TILE");   // measurement knob (A/B runs only)
   int eth = 0, etw = 0;
   if (tile_env) sscanf(tile_env, "%dx%d", &eth, &etw);
   double best = 1e300;
@@ -1777,7 +1777,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     // channel groups: enough workgroups to fill the chip when the batch is small, ~4 per CU (each
     // walks its channels one memory round trip at a time; B=16 128^2 32ch bwd: 2 per CU 1.456,
     // 4 1.382, 8 1.392, 16 1.411 ms; tools/bc_sweep.sh)
-    static const char* ncg_env = getenv("GNCA_BC_WGS_PER_CU");   // measurement knob (A/B runs only)
+    static const char* ncg_env = GNCA_AB_ENV("GNCA_BC_WGS_PER_CU");   // measurement knob (A/B runs only)
     const long per_cu = ncg_env && atoi(ncg_env) > 0 ? atoi(ncg_env) : 4;
     const long wgs = (long)B * P.tps3, want = per_cu * bwd_device_cus();
     a.ncg = (int)std::min<long>(C, std::max<long>(1, (want + wgs - 1) / wgs));

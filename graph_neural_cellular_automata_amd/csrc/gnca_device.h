@@ -16,6 +16,15 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
 
+// Environment knobs that change kernel selection or geometry exist only in measurement builds
+// (-DGNCA_AB_KNOBS, tools/ A/B scripts): in the shipped library the environment cannot change
+// which product kernel runs.
+#ifdef GNCA_AB_KNOBS
+#define GNCA_AB_ENV(name) getenv(name)
+#else
+#define GNCA_AB_ENV(name) ((const char*)nullptr)
+#endif
+
 __device__ __forceinline__ int wrapi(int v, int n) {
   v %= n;
   return v < 0 ? v + n : v;

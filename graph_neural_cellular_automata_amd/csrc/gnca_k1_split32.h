@@ -1,8 +1,8 @@
 // gnca_k1_split32.h — K1 of the 32-channel / hidden-128 step (BASELINE config 5: 128^2, r = 5,
 // K = 16) on bf16 MFMA with the exact 3-way fp32 splits of gnca_k1_split.h (included after it).
 //
-// Why.  The fp32-MFMA two-phase K1 (gnca_k1_2ph) spends 17 K of its 52 K cycles per 16x16 tile in
-// fp32 MFMA issue (1/16 of the bf16 rate, on the VALU datapath).  Here every product is six exact
+// Why.  Round 1's fp32-MFMA two-phase K1 (since removed) spent 17 K of its 52 K cycles per 16x16
+// tile in fp32 MFMA issue (1/16 of the bf16 rate, on the VALU datapath).  Here every product is six exact
 // bf16 products (numerics as gnca_k1_split.h: fp32-class, dropped terms <= 2^-24 |a||b| each).
 //
 // Tile pipeline: 16x16 tiles, the region's channel planes staged in two 16-channel phases through

@@ -841,465 +841,6 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// K1 for 32-channel states (BASELINE config 5: 32 ch, 128^2, r = 5, K = 16), two channel phases.
-// gnca_k1_update stages every channel of the tile + halo at once; at C = 32 the weight fragments
-// alone take 87 KB of LDS, which leaves room for 8x16 tiles only (runtime-geometry variant: 1.41
-// ms per B=128 launch, 29 % of it LDS-DMA issue).  Here the channel planes go through ONE 16-channel
-// buffer in two phases: phase 0 stages channels 0-15 (+ the alpha ring), builds the planes and the
-// live-cell list and runs the GEMM1 / message k-steps that read those channels; phase 1 stages
-// channels 16-31 and finishes them, then ReLU, GEMM2 and the epilogue.  Each wave's groups (at
-// most GPW per tile) keep their GEMM1 / message accumulators in registers across the phases.
-// Same arithmetic as gnca_k1_update; GEMM1's k-steps are accumulated phase by phase (channels
-// 0-15 of every feature block, then 16-31), so fp32 rounding differs from the runtime-geometry
-// variant at the ulp level (the oracle tolerance, not bitwise).
-// ------------------------------------------------------------------------------------------
-struct K1L2 {
-  int xs, sp, al, kp, lst, b1s, bms, percs, red, wmf, w2f, w1f, total;
-};
-
-__host__ __device__ constexpr int k1l2_pstr(int RH, int RW) { return 64 * ((RH * RW + 63) / 64) + 16; }
-
-__host__ __device__ inline K1L2 k1_2ph_layout(int CP, int HDP, int TH, int TW, int RY, int RX) {
-  K1L2 L{};
-  const int CPQ = CP / 4, KS = 3 * CPQ, MT = HDP / 16, MO = (CP + 15) / 16;
-  const int RH = TH + 2 * RY, RW = TW + 2 * RX;
-  const int NIA = ((RH + 2) * (RW + 2) + 63) / 64;
-  int o = 0;
-  L.xs = o; o += (CP / 2) * k1l2_pstr(RH, RW);
-  L.sp = o; o += r4(RH * RW);
-  L.al = o; o += 64 * NIA;
-  L.kp = o; o += r4(TH * TW);
-  L.lst = o; o += r4(TH * TW) + 16;
-  L.b1s = o; o += r4(HDP);
-  L.bms = o; o += r4(CP);
-  L.percs = o; o += CP * 36;
-  L.red = o; o += 64;
-  L.wmf = o; o += MO * 64 * odd4(CPQ);
-  L.w2f = o; o += MO * 64 * odd4(4 * MT);
-  L.w1f = o; o += MT * 64 * odd4(KS);
-  L.total = o;
-  return L;
-}
-
-template <int CP, int HDP, int TH, int TW, int RY, int RX, int KU>
-__global__ __launch_bounds__(512, 1) void gnca_k1_2ph(const K1Args a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int NT = 512, NW = NT / 64;
-  constexpr int CPQ = CP / 4, KS = 3 * CPQ, MT = HDP / 16, MO = CP / 16;
-  constexpr int CH = CP / 2, CHQ = CPQ / 2;            // channels / t-values per phase
-  constexpr int KSP = odd4(KS), S2r = 4 * MT, S2 = odd4(S2r), SWM = odd4(CPQ);
-  constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX;
-  constexpr int NI = (RH * RW + 63) / 64, PSTR = k1l2_pstr(RH, RW);
-  constexpr int ALW = RW + 2, NIA = ((RH + 2) * ALW + 63) / 64;
-  constexpr int ncell = TH * TW, NG = ncell / 16, GPW = (NG + NW - 1) / NW;
-  constexpr bool graph_on = KU > 0;
-  static_assert(CP % 32 == 0 && ncell % 16 == 0 && CHQ % 4 == 0, "K1-2ph geometry");
-  const K1L2 L = k1_2ph_layout(CP, HDP, TH, TW, RY, RX);
-  float* w1f = smem + L.w1f;
-  float* w2f = smem + L.w2f;
-  float* wmf = smem + L.wmf;
-  float* b1s = smem + L.b1s;
-  float* bms = smem + L.bms;
-  float* percs = smem + L.percs;
-  float* fp = smem + L.kp;
-  float* red = smem + L.red;
-  float* xs = smem + L.xs;
-  float* al = smem + L.al;
-  float* sp = smem + L.sp;
-  int* lst = reinterpret_cast<int*>(smem + L.lst);
-  int* wcnt = lst + r4(ncell);
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int g = lane >> 4, c16 = lane & 15;
-  constexpr int C = CP;
-  const int H = a.H, W = a.W, Hd = a.hidden;
-  const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
-  const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
-  const float thr = a.alpha_thr, gthr = a.graph_alpha_thr;
-  const size_t HW = (size_t)H * W;
-
-  // ---- weights -> LDS in MFMA fragment order, every load in flight before the first store ----
-  {
-    RegFill<NT, MT * 64 * KSP> fw1;
-    RegFill<NT, MO * 64 * S2> fw2;
-    RegFill<NT, HDP> fb1;
-    RegFill<NT, CP * 36> fpc;
-    RegFill<NT, MO * 64 * SWM> fwm;
-    RegFill<NT, CP> fbm;
-    fw1.load(tid, [&](int idx) {
-      const int s_ = idx % KSP, ml = idx / KSP, l = ml & 63, m = ml >> 6;
-      const int hid = 16 * m + (l & 15), slot = 4 * s_ + (l >> 4);
-      const int f = slot / CP, c = slot - f * CP;
-      return (s_ < KS && hid < Hd) ? a.w1[(size_t)hid * 3 * C + f * C + c] : 0.f;
-    });
-    fw2.load(tid, [&](int idx) {
-      const int e = idx % S2, ml = idx / S2, l = ml & 63, mo = ml >> 6;
-      const int m = e >> 2, r = e & 3;
-      const int co = 16 * mo + (l & 15), hid = 16 * m + 4 * (l >> 4) + r;
-      return (e < S2r && hid < Hd) ? a.w2[(size_t)co * Hd + hid] : 0.f;
-    });
-    fb1.load(tid, [&](int idx) { return idx < Hd ? a.b1[idx] : 0.f; });
-    fpc.load(tid, [&](int idx) {
-      const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
-      return tap < 9 ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
-    });
-    fwm.load(tid, [&](int idx) {
-      const int s_ = idx % SWM, ml = idx / SWM, l = ml & 63, mo = ml >> 6;
-      const int co = 16 * mo + (l & 15), c = 4 * s_ + (l >> 4);
-      return (graph_on && s_ < CPQ) ? a.wm[co * C + c] : 0.f;
-    });
-    fbm.load(tid, [&](int idx) { return graph_on ? a.bm[idx] : 0.f; });
-    fw1.store(w1f, tid);
-    fw2.store(w2f, tid);
-    fb1.store(b1s, tid);
-    fpc.store(percs, tid);
-    fwm.store(wmf, tid);
-    fbm.store(bms, tid);
-  }
-  __syncthreads();
-  bool sobel;
-  {
-    int ok = 1;
-    for (int idx = tid; idx < C * 27; idx += NT) {
-      const int c = idx / 27, e = idx % 27, f = e / 9, tap = e % 9;
-      const int tr = tap / 3, tc = tap % 3;
-      float ref;
-      if (f == 0) ref = (tap == 4) ? 1.f : 0.f;
-      else if (f == 1) ref = (float)((tc == 0 ? 1 : (tc == 2 ? -1 : 0)) * (tr == 1 ? 2 : 1));
-      else ref = (float)((tr == 0 ? 1 : (tr == 2 ? -1 : 0)) * (tc == 1 ? 2 : 1));
-      if (percs[c * 36 + f * 12 + tap] != ref) ok = 0;
-    }
-    sobel = __syncthreads_and(ok) != 0;
-  }
-  // W_M fragments and b_M stay in LDS (read where used: registers are the limit here)
-  float gainr[MO];
-#pragma unroll
-  for (int mo = 0; mo < MO; ++mo)
-    gainr[mo] = (graph_on && !(hidden_only && mo == 0 && g == 0)) ? a.message_gain : 0.f;
-
-  const int nxcd = gridDim.x >= 8 ? 8 : 1;
-  const int xg_ = blockIdx.x % nxcd, xr_ = blockIdx.x / nxcd;
-  const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
-  const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
-  const int t_begin = xg_ * tq + min(xg_, trm), t_end = t_begin + tq + (xg_ < trm ? 1 : 0);
-  for (int tile = t_begin + xr_; tile < t_end; tile += per_x) {
-    const int b = tile / a.tps, tin = tile - b * a.tps;
-    const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
-    const int i0 = ty * TH, j0 = tx * TW;
-    const float* xb = a.x + (size_t)b * C * HW;
-    if (a.active && !a.active[b]) {
-      if (tid < 2 * NW) a.stats[(size_t)tile * 2 * NW + tid] = 0.0;
-      continue;
-    }
-    const size_t cell0 = (size_t)i0 * W + j0;
-    // channel planes [ph*CH, ph*CH + CH) of the (RH x RW) region -> xs (torus-wrapped)
-    auto stage = [&](int ph) {
-#pragma unroll 1
-      for (int ii_ = wave; ii_ < NI; ii_ += NW) {
-        const int e = 64 * ii_ + lane;
-        int off = 0;
-        if (e < RH * RW) {
-          const int vr = e / RW, vc = e - (e / RW) * RW;
-          int ii = i0 - RY + vr, jj = j0 - RX + vc;
-          ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
-          jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-          off = ii * W + jj;
-        }
-        const float* src0 = xb + (size_t)(ph * CH) * HW + off;
-        float* dst = xs + 64 * ii_;
-#pragma unroll 4
-        for (int c = 0; c < CH; ++c)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (size_t)c * HW),
-                                           (__attribute__((address_space(3))) void*)(dst + c * PSTR), 4, 0, 0);
-      }
-    };
-    __syncthreads();   // previous tile's readers of xs / lst are done
-    stage(0);
-    if (a.alive) {
-      // the previous K2's alive bytes over the region, one byte -> one dword per position
-      // (SURVEY a13), instead of the alpha plane with its extra ring
-      const uint8_t* ab = a.alive + (size_t)b * HW;
-#pragma unroll 1
-      for (int ii_ = wave; ii_ < NI; ii_ += NW) {
-        const int e = 64 * ii_ + lane;
-        int off = 0;
-        if (e < RH * RW) {
-          const int vr = e / RW, vc = e - (e / RW) * RW;
-          int ii = i0 - RY + vr, jj = j0 - RX + vc;
-          ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
-          jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-          off = ii * W + jj;
-        }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ab + off),
-                                         (__attribute__((address_space(3))) void*)(al + 64 * ii_), 1, 0, 0);
-      }
-    } else
-#pragma unroll 1
-    for (int ii_ = wave; ii_ < NIA; ii_ += NW) {
-      const int e = 64 * ii_ + lane;
-      int off = 0;
-      if (e < (RH + 2) * ALW) {
-        const int vr = e / ALW, vc = e - (e / ALW) * ALW;
-        int ii = i0 - RY - 1 + vr, jj = j0 - RX - 1 + vc;
-        ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
-        jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-        off = ii * W + jj;
-      }
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xb + 3 * HW + off),
-                                       (__attribute__((address_space(3))) void*)(al + 64 * ii_), 4, 0, 0);
-    }
-#pragma unroll 1
-    for (int n = tid; n < ncell; n += NT) {
-      const int ti = n / TW, tj = n - (n / TW) * TW;
-      const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
-      bool fire = true;
-      if (a.fire_mode == GNCA_FIRE_RAND_F32)
-        fire = reinterpret_cast<const float*>(a.fire)[(size_t)b * HW + cell] <= a.fire_rate;
-      else if (a.fire_mode == GNCA_FIRE_MASK_U8)
-        fire = reinterpret_cast<const uint8_t*>(a.fire)[(size_t)b * HW + cell] != 0;
-      else if (a.fire_mode == GNCA_FIRE_HASH)
-        fire = hash_uniform(a.seed, a.rng_step, (uint64_t)(a.sample_base + b), cell) <= a.fire_rate;
-      fp[n] = fire ? 1.f : 0.f;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // sender plane over the region; keep = pre-alive AND fire over the tile
-    if (a.alive) {
-      const int* alw = reinterpret_cast<const int*>(al);
-#pragma unroll 1
-      for (int pos = tid; pos < RH * RW; pos += NT) {
-        const int vr = pos / RW, vc = pos - (pos / RW) * RW;
-        const int v = alw[pos] & 0xff;
-        sp[pos] = a2a ? (float)((v >> 1) & 1) : 1.f;
-        const int ti = vr - RY, tj = vc - RX;
-        if (ti >= 0 && ti < TH && tj >= 0 && tj < TW) {
-          const int n = ti * TW + tj;
-          fp[n] = (v & 1) ? fp[n] : 0.f;
-        }
-      }
-    } else
-#pragma unroll 1
-    for (int pos = tid; pos < RH * RW; pos += NT) {
-      const int vr = pos / RW, vc = pos - (pos / RW) * RW;
-      int iq = i0 - RY + vr, jq = j0 - RX + vc;
-      iq = iq < 0 ? iq + H : (iq >= H ? iq - H : iq);
-      jq = jq < 0 ? jq + W : (jq >= W ? jq - W : jq);
-      const float* q = al + (vr + 1) * ALW + (vc + 1);
-      const float NEG = -INFINITY;
-      const bool up = iq > 0, dn = iq < H - 1, lf = jq > 0, rt = jq < W - 1;
-      const float mu_ = fmaxf(fmaxf(lf ? q[-ALW - 1] : NEG, q[-ALW]), rt ? q[-ALW + 1] : NEG);
-      const float mm_ = fmaxf(fmaxf(lf ? q[-1] : NEG, q[0]), rt ? q[1] : NEG);
-      const float md_ = fmaxf(fmaxf(lf ? q[ALW - 1] : NEG, q[ALW]), rt ? q[ALW + 1] : NEG);
-      const float mx = fmaxf(fmaxf(up ? mu_ : NEG, mm_), dn ? md_ : NEG);
-      sp[pos] = a2a ? (mx > gthr ? 1.f : 0.f) : 1.f;
-      const int ti = vr - RY, tj = vc - RX;
-      if (ti >= 0 && ti < TH && tj >= 0 && tj < TW) {
-        const int n = ti * TW + tj;
-        fp[n] = mx > thr ? fp[n] : 0.f;
-      }
-    }
-    __syncthreads();
-    // live-cell compaction (cell order, deterministic); dead cells get dx = 0
-    int nlive = 0;
-    for (int n0 = 0; n0 < ncell; n0 += NT) {
-      const int n = n0 + tid;
-      const bool inb = n < ncell;
-      const bool live = inb && fp[n] != 0.f;
-      const uint64_t bal = __ballot(live);
-      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-      if (lane == 0) wcnt[wave] = __popcll(bal);
-      __syncthreads();
-      int off = nlive, tot = 0;
-#pragma unroll
-      for (int w_ = 0; w_ < NW; ++w_) {
-        off += w_ < wave ? wcnt[w_] : 0;
-        tot += wcnt[w_];
-      }
-      if (live) {
-        lst[off + pre] = n;
-      } else if (inb) {
-        const int ti = n / TW, tj = n - (n / TW) * TW;
-        float* oz = a.out + (size_t)b * C * HW + cell0 + (size_t)ti * W + tj;
-#pragma unroll
-        for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
-      }
-      nlive += tot;
-      __syncthreads();
-    }
-    const int ngrp = (nlive + 15) >> 4;
-
-    // ---- the two channel phases; a wave's groups q = wave + NW*gi keep their accumulators ----
-    f4 acc[GPW][MT], accm[GPW][MO];
-    float Sg[GPW], ps1[GPW], ps2[GPW];
-#pragma unroll
-    for (int gi = 0; gi < GPW; ++gi) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m) acc[gi][m] = *reinterpret_cast<const f4*>(b1s + 16 * m + 4 * g);
-#pragma unroll
-      for (int mo = 0; mo < MO; ++mo) accm[gi][mo] = f4{0.f, 0.f, 0.f, 0.f};
-      Sg[gi] = 0.f;
-      ps1[gi] = 0.f;
-      ps2[gi] = 0.f;
-    }
-#pragma unroll
-    for (int ph = 0; ph < 2; ++ph) {
-      if (ph == 1) {
-        __syncthreads();   // every wave is done with phase 0's planes
-        stage(1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      }
-#pragma unroll
-      for (int gi = 0; gi < GPW; ++gi) {
-        const int q = wave + NW * gi;
-        if (q >= ngrp) continue;   // wave-uniform
-        int n = 16 * q + c16;
-        const bool valid = n < nlive;
-        n = lst[valid ? n : 0];
-        const int ti = n / TW, tj = n - (n / TW) * TW;
-        const int pidx = (RY + ti) * RW + (RX + tj);
-        const float* xg = xs + g * PSTR;
-        float gv[CHQ];
-#pragma unroll
-        for (int t = 0; t < CHQ; ++t) gv[t] = 0.f;
-        if constexpr (graph_on) {
-          float S = 0.f;
-          const float* spq = sp + pidx;
-          const float* xq = xg + pidx;
-#pragma unroll
-          for (int o = 0; o < KU; ++o) {
-            const int d = a.odl[o];
-            const float s_ = spq[-d];
-            S += s_;
-            const float* xo = xq - d;
-#pragma unroll
-            for (int t = 0; t < CHQ; ++t) gv[t] = fmaf(s_, xo[4 * t * PSTR], gv[t]);
-          }
-          const float wu = a.uniform_w;
-#pragma unroll
-          for (int t = 0; t < CHQ; ++t) gv[t] *= wu;
-          if (ph == 0) Sg[gi] = S * wu;
-        }
-        float y[3][CHQ];
-        {
-          const int ic = i0 + ti, jc = j0 + tj;
-          const bool up = ic > 0, dn = ic < H - 1, lf = jc > 0, rt = jc < W - 1;
-#pragma unroll
-          for (int t = 0; t < CHQ; ++t) {
-            const float* xc = xg + 4 * t * PSTR + pidx;
-            float n0 = xc[-RW - 1], n1 = xc[-RW], n2 = xc[-RW + 1];
-            float n3 = xc[-1], n4 = xc[0], n5 = xc[1];
-            float n6 = xc[RW - 1], n7 = xc[RW], n8 = xc[RW + 1];
-            n0 = (up && lf) ? n0 : 0.f; n1 = up ? n1 : 0.f; n2 = (up && rt) ? n2 : 0.f;
-            n3 = lf ? n3 : 0.f;                               n5 = rt ? n5 : 0.f;
-            n6 = (dn && lf) ? n6 : 0.f; n7 = dn ? n7 : 0.f; n8 = (dn && rt) ? n8 : 0.f;
-            if (sobel) {
-              y[0][t] = n4;
-              y[1][t] = (fmaf(2.f, n3, n0) + n6) - (fmaf(2.f, n5, n2) + n8);
-              y[2][t] = (fmaf(2.f, n1, n0) + n2) - (fmaf(2.f, n7, n6) + n8);
-            } else {
-              const int c = CH * ph + 4 * t + g;
-              const f4* pw = reinterpret_cast<const f4*>(percs + c * 36);
-#pragma unroll
-              for (int f = 0; f < 3; ++f) {
-                const f4 w0 = pw[3 * f], w1 = pw[3 * f + 1], w2 = pw[3 * f + 2];
-                float ac = w0[0] * n0;
-                ac = fmaf(w0[1], n1, ac); ac = fmaf(w0[2], n2, ac); ac = fmaf(w0[3], n3, ac);
-                ac = fmaf(w1[0], n4, ac); ac = fmaf(w1[1], n5, ac); ac = fmaf(w1[2], n6, ac);
-                ac = fmaf(w1[3], n7, ac); ac = fmaf(w2[0], n8, ac);
-                y[f][t] = ac;
-              }
-            }
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (graph_on) {
-#pragma unroll
-          for (int t = 0; t < CHQ; ++t)
-#pragma unroll
-            for (int mo = 0; mo < MO; ++mo)
-              accm[gi][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wmf[(mo * 64 + lane) * SWM + CHQ * ph + t], gv[t],
-                                                                  accm[gi][mo], 0, 0, 0);
-        }
-        // GEMM1 k-steps of this phase's channels: s = f*CPQ + CHQ*ph + t (quad-aligned runs)
-#pragma unroll
-        for (int f = 0; f < 3; ++f) {
-          const int s0 = f * CPQ + CHQ * ph;
-#pragma unroll
-          for (int tq = 0; tq < CHQ; tq += 4) {
-            f4 w4[MT];
-#pragma unroll
-            for (int m = 0; m < MT; ++m) w4[m] = *reinterpret_cast<const f4*>(w1f + (m * 64 + lane) * KSP + s0 + tq);
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-              for (int m = 0; m < MT; ++m)
-                acc[gi][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[m][u], y[f][tq + u], acc[gi][m], 0, 0, 0);
-          }
-        }
-        if (ph == 0) continue;
-        // -- ReLU, GEMM2, epilogue --
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[gi][m][r] = relu_nan(acc[gi][m][r]);
-        f4 acc2[2][MO];
-#pragma unroll
-        for (int mo = 0; mo < MO; ++mo) {
-          acc2[0][mo] = f4{0.f, 0.f, 0.f, 0.f};
-          acc2[1][mo] = f4{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          f4 w2v[MO];
-#pragma unroll
-          for (int mo = 0; mo < MO; ++mo) w2v[mo] = *reinterpret_cast<const f4*>(w2f + (mo * 64 + lane) * S2 + 4 * m);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int mo = 0; mo < MO; ++mo)
-              acc2[r & 1][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2v[mo][r], acc[gi][m][r], acc2[r & 1][mo], 0, 0, 0);
-        }
-        const int relcell = ti * W + tj;
-        float* ob = a.out + ((size_t)b * C + 4 * g) * HW + cell0;
-        float s1 = 0.f, s2 = 0.f;   // this group's GroupNorm partials
-#pragma unroll
-        for (int mo = 0; mo < MO; ++mo)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = acc2[0][mo][r] + acc2[1][mo][r];
-            if (graph_on) v = fmaf(fast_tanh(fmaf(bms[16 * mo + 4 * g + r], Sg[gi], accm[gi][mo][r])), gainr[mo], v);
-            if (!valid) continue;
-            ob[(16 * mo + r) * HW + relcell] = v;
-            s1 += v;
-            s2 = fmaf(v, v, s2);
-          }
-        ps1[gi] = s1;
-        ps2[gi] = s2;
-      }
-    }
-    // ---- per-(tile, wave) GroupNorm partials ----
-    float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-    for (int gi = 0; gi < GPW; ++gi)
-      if (wave + NW * gi < ngrp) {
-        t1 += ps1[gi];
-        t2 += ps2[gi];
-      }
-    double d1 = t1, d2 = t2;
-    for (int off = 32; off > 0; off >>= 1) {
-      d1 += __shfl_xor(d1, off);
-      d2 += __shfl_xor(d2, off);
-    }
-    if (lane == 0) {   // per-(tile, wave) partials, as gnca_k1_update
-      a.stats[((size_t)tile * NW + wave) * 2 + 0] = d1;
-      a.stats[((size_t)tile * NW + wave) * 2 + 1] = d2;
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // K2: GroupNorm + tanh*gain + residual + post-update alpha gate
 // ------------------------------------------------------------------------------------------
 struct K2Args {
@@ -1769,25 +1310,21 @@ struct Variant {
   int CP, HDP, TH, TW, RY, RX, KU;   // TH == 0: runtime geometry (generic)
   const void* fn;
   int NT;                            // threads per workgroup
-  int ph2;                           // 1: gnca_k1_2ph (channels staged in two phases)
   int split;                         // 1: gnca_k1_split, 2: gnca_k1_split32 (bf16 MFMA on exact 3-way splits)
   int lds_split;                     // its LDS bytes (compile-time layout)
 };
 
-#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0, 0}
-#define GNCA_FV(cp, hd, th, tw, ry, rx, ku, nt) \
-  {cp, hd, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, th, tw, ry, rx, ku, nt>), nt, 0, 0, 0}
-#define GNCA_2V(cp, hd, th, tw, ry, rx, ku) \
-  {cp, hd, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_2ph<cp, hd, th, tw, ry, rx, ku>), 512, 1, 0, 0}
+#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0}
 #define GNCA_SV(th, tw, ry, rx, ku) \
-  {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), 512, 0, 1, \
+  {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), 512, 1, \
    ks_layout<th, tw, ry, rx>().total}
 #define GNCA_S32V(th, tw, ry, rx, ku) \
-  {32, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split32<th, tw, ry, rx, ku>), 512, 0, 2, \
+  {32, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split32<th, tw, ry, rx, ku>), 512, 2, \
    ks32_layout<th, tw, ry, rx>().total}
 static const Variant kVariants[] = {
-    // 16 channels, hidden 128, bf16 MFMA on exact 3-way splits (gnca_k1_split.h): preferred over
-    // the fp32-MFMA variants of the same shape class (GNCA_K1_F32=1 selects those instead)
+    // 16 channels, hidden 128, bf16 MFMA on exact 3-way splits (gnca_k1_split.h), compile-time
+    // geometry: list order is the large-batch preference (24x36: the largest tiles whose halo fits
+    // LDS, 1.6x halo re-read); 8x24 / 8x20 serve small batches and the trainer's 40^2 canvas
     GNCA_SV(24, 36, 4, 4, 8),
     GNCA_SV(36, 24, 4, 4, 8),
     GNCA_SV(24, 24, 4, 4, 8),
@@ -1796,26 +1333,9 @@ static const Variant kVariants[] = {
     GNCA_SV(8, 20, 4, 4, 8),
     GNCA_SV(8, 20, 1, 4, 0),
     // 32 channels (BASELINE config 5: 128^2, r = 5, K = 16): 16x16 tiles, channel planes staged
-    // in two 16-channel phases; bf16 split MFMA (gnca_k1_split32.h), then the fp32-MFMA
-    // gnca_k1_2ph (GNCA_K1_F32=1); graph and no-message steps
+    // in two 16-channel phases (gnca_k1_split32.h); graph and no-message steps
     GNCA_S32V(16, 16, 5, 5, 16),
     GNCA_S32V(16, 16, 1, 1, 0),
-    GNCA_2V(32, 128, 16, 16, 5, 5, 16),
-    GNCA_2V(32, 128, 16, 16, 1, 1, 0),
-    // compile-time geometry: the benchmark / trainer shapes (16 ch, hidden 128, 8x24 tiles)
-    // graph, torus, r <= 4, K = 8 (the benchmark / trainer shape class): one 512-thread workgroup
-    // per CU (8 waves share one copy of the weight fragments), the largest tiles whose halo fits
-    // LDS (24x36: 1.6x halo re-read; measured 24x24 0.72 ms, 24x36 0.68 ms per B=1024 72^2 launch)
-    GNCA_FV(16, 128, 24, 36, 4, 4, 8, 512),
-    GNCA_FV(16, 128, 36, 24, 4, 4, 8, 512),
-    GNCA_FV(16, 128, 24, 24, 4, 4, 8, 512),
-    GNCA_FV(16, 128, 8, 24, 4, 4, 8, 256),    // same, 8x24 tiles, 2 WGs / CU
-    GNCA_FV(16, 128, 8, 24, 4, 4, 8, 512),    // small batches: 8 waves per 8x24 tile (<= 1 group each)
-    GNCA_FV(16, 128, 8, 24, 1, 1, 0, 256),    // classic NCA (no gather)
-    GNCA_FV(16, 128, 8, 24, 1, 1, 0, 512),
-    // the trainer's canvas (config.json img_size 40): 8x20 tiles, graph and no-message steps
-    GNCA_FV(16, 128, 8, 20, 4, 4, 8, 512),
-    GNCA_FV(16, 128, 8, 20, 1, 1, 0, 512),
     // runtime geometry: every other shape class
     GNCA_GV(4, 32),   GNCA_GV(4, 64),   GNCA_GV(4, 128),  GNCA_GV(8, 32),   GNCA_GV(8, 64),
     GNCA_GV(8, 128),  GNCA_GV(12, 64),  GNCA_GV(12, 128), GNCA_GV(16, 32),  GNCA_GV(16, 64),
@@ -1823,8 +1343,6 @@ static const Variant kVariants[] = {
     GNCA_GV(32, 64),  GNCA_GV(32, 128),
 };
 #undef GNCA_GV
-#undef GNCA_FV
-#undef GNCA_2V
 #undef GNCA_SV
 #undef GNCA_S32V
 
@@ -1879,29 +1397,21 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->RX = rx;
   const int CP = P->var->CP, HDP = P->var->HDP;
   const bool attn_on = attn && P->graph_on;
-  // a compile-time-geometry instantiation, when the shape allows one
-  // measurement knobs (A/B runs only): GNCA_K1_NT256 skips the 512-thread variants,
+  // a compile-time-geometry instantiation (the bf16-split K1s), when the shape allows one;
+  // GNCA_AB_ENV knobs exist only in -DGNCA_AB_KNOBS measurement builds (gnca_device.h):
   // GNCA_K1_TILE=<TH>x<TW> restricts the fixed variants to one tile shape
-  static const bool only256 = getenv("GNCA_K1_NT256") != nullptr;
-  static const bool no_split = getenv("GNCA_K1_F32") != nullptr && atoi(getenv("GNCA_K1_F32")) != 0;
-  static const char* tile_env = getenv("GNCA_K1_TILE");
+  static const char* tile_env = GNCA_AB_ENV("GNCA_K1_TILE");
   const Variant* fixed_pick = nullptr;
   long fixed_tiles = 0;
   for (const Variant& v : kVariants) {
     if (v.TH == 0 || v.CP != CP || v.HDP != HDP || d->C != CP || msg_only || attn_on) continue;
-    if (only256 && v.NT > kThreads) continue;
-    if (no_split && v.split) continue;
     if (tile_env) {
       int th = 0, tw = 0;
       if (sscanf(tile_env, "%dx%d", &th, &tw) == 2 && (th != v.TH || tw != v.TW)) continue;
     }
     if (d->H % v.TH || d->W % v.TW || ry > v.RY || rx > v.RX) continue;
     if (v.KU > 0 ? !(P->graph_on && !zp && !P->need_k0 && P->k == v.KU) : P->graph_on) continue;
-    const int ltot = v.split ? v.lds_split / 4
-                     : v.ph2 ? k1_2ph_layout(CP, HDP, v.TH, v.TW, v.RY, v.RX).total
-                             : k1_layout(CP, HDP, v.TH, v.TW, v.RY, v.RX, P->k).total;
-    // LDS per workgroup: 80 KB for two 256-thread workgroups per CU, 160 KB for one of 512
-    if ((size_t)ltot * 4 > (v.NT >= 512 ? (size_t)max_lds_bytes() : 80 * 1024)) continue;
+    if ((size_t)v.lds_split > (size_t)max_lds_bytes()) continue;
     // list order is the large-batch preference (big tiles amortise the per-tile work); a batch
     // too small to give every CU two workgroups' worth of tiles takes the variant with the most
     // tiles instead (measured at B=8, 72^2: 24x36 55 us/step, 8x24 43 us/step)
@@ -1911,10 +1421,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
       fixed_pick = &v;
       fixed_tiles = tiles;
       if (tiles >= fill) break;   // large batch: first (preferred) eligible variant
-    } else if (tiles > fixed_tiles ||
-               // same tile count and every tile gets a CU of its own: the wider workgroup
-               // (fewer 16-cell groups per wave: a shorter tile latency)
-               (tiles == fixed_tiles && tiles <= device_cus() && v.NT > fixed_pick->NT)) {
+    } else if (tiles > fixed_tiles) {
       fixed_pick = &v;
       fixed_tiles = tiles;
     }
@@ -1935,9 +1442,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   if (P->var->TH) {
     bth = P->var->TH;
     btw = P->var->TW;
-    blds = P->var->split ? (size_t)P->var->lds_split
-                         : (size_t)(P->var->ph2 ? k1_2ph_layout(CP, HDP, bth, btw, ry, rx).total
-                                                : k1_layout(CP, HDP, bth, btw, ry, rx, P->k).total) * 4;
+    blds = (size_t)P->var->lds_split;
   }
   for (int pass = 0; pass < 2 && !bth; ++pass) {
     const size_t cap = pass == 0 ? 80 * 1024 : (size_t)max_lds_bytes();
@@ -1973,7 +1478,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
     const bool thin = (long)d->W * d->C <= 96L * 16;
     const long nb_target = std::max<long>(thin ? (d->H + 3) / 4 : 6, (2L * device_cus() + d->B - 1) / d->B);
     long rows = (d->H + nb_target - 1) / nb_target;
-    static const char* band_env = getenv("GNCA_K2_BAND");   // measurement knob (A/B runs only)
+    static const char* band_env = GNCA_AB_ENV("GNCA_K2_BAND");   // measurement knob (A/B runs only)
     if (band_env && atoi(band_env) > 0) rows = atoi(band_env);
     const long cap = (48L * 1024 / 4 / d->W - 2) / 2;
     if (rows > cap) rows = cap;
@@ -2003,7 +1508,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
     // 0.233, 8 0.180, 12 0.170, 24 0.170 ms; since the alpha plane is dense: 6 0.164, 8 0.158,
     // 12 0.161, 24 0.163 ms, within the box-to-box spread)
     long rows = 12;
-    static const char* band_env = getenv("GNCA_K2_BAND");   // measurement knob (A/B runs only)
+    static const char* band_env = GNCA_AB_ENV("GNCA_K2_BAND");   // measurement knob (A/B runs only)
     if (band_env && atoi(band_env) > 0) rows = atoi(band_env);
     const long cap = (48L * 1024 / 4 / d->W - 2) / 2;
     rows = std::max(1L, std::min(rows, cap));
@@ -2232,9 +1737,10 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   k2.gthr = d->graph_alpha_thr;
   k2.alive_out = alive_out ? alive : nullptr;
   k2.active = active;
-  // GNCA_K2_ZIGZAG=0 (A/B runs only) keeps the plain sample order; measured B=1024: 0.690 -> 0.679
-  // ms/step (K2 0.182 -> 0.180 ms, the next K1 -0.5 %)
-  static const bool zz = getenv("GNCA_K2_ZIGZAG") == nullptr || atoi(getenv("GNCA_K2_ZIGZAG")) != 0;
+  // GNCA_K2_ZIGZAG=0 (measurement builds only) keeps the plain sample order; measured B=1024: 0.690
+  // -> 0.679 ms/step (K2 0.182 -> 0.180 ms, the next K1 -0.5 %)
+  static const char* zz_env = GNCA_AB_ENV("GNCA_K2_ZIGZAG");
+  static const bool zz = zz_env == nullptr || atoi(zz_env) != 0;
   k2.zigzag = zz ? 1 : 0;
   if (compact) {
     k2.rmask = rmask;
@@ -2295,8 +1801,6 @@ int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* 
   if (v->split)
     snprintf(name, (size_t)n, "gnca_k1_split%s<%d,%d,%d,%d,%d>", v->split == 2 ? "32" : "", v->TH, v->TW, v->RY,
              v->RX, v->KU);
-  else if (v->ph2)
-    snprintf(name, (size_t)n, "gnca_k1_2ph<%d,%d,%d,%d,%d,%d,%d>", v->CP, v->HDP, v->TH, v->TW, v->RY, v->RX, v->KU);
   else
     snprintf(name, (size_t)n, "gnca_k1_update<%d,%d,%d,%d,%d,%d,%d,%d>", v->CP, v->HDP, v->TH, v->TW, v->RY, v->RX,
              v->KU, v->NT);

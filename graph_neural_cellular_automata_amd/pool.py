@@ -10,13 +10,17 @@ whole C4 pool (1024 x 16 x 72 x 72 fp32 = 340 MB) stays resident.
 Multi-GPU (``shard=(rank, world)``): each rank keeps only its contiguous slice of the pool
 (``sharding.shard_range``) and samples its share of the batch from it.  Every rank still calls
 ``seed_fn`` for all P samples, so the global RNG streams stay identical across ranks.  A sharded
-pool draws its slot indices from its own ``random.Random`` (seeded per rank), not from the global
-stream: slices may differ in length by one, and ``random.sample`` over different lengths consumes
-the stream differently, which would desynchronise the per-step offset draws that every rank must
-share (``sharding.py``).
+pool draws its slot indices from its own ``random.Random``, not from the global stream: slices may
+differ in length by one, and ``random.sample`` over different lengths consumes the stream
+differently, which would desynchronise the per-step offset draws that every rank must share
+(``sharding.py``).  That private stream is seeded from the global stream's STATE at construction
+(read, not consumed: identical on every rank, and it follows the user's ``random.seed``) mixed
+with the rank; ``rng_state()`` / ``set_rng_state()`` carry it through a checkpoint
+(``checkpoint.save_checkpoint(..., pool=)``).
 """
 from __future__ import annotations
 
+import hashlib
 import random
 
 import torch
@@ -38,7 +42,11 @@ class SamplePool:
                 seeds.append(s.reshape(s.shape[-3:]).to(device))
         self.states = torch.stack(seeds).contiguous() if seeds else torch.empty(0, device=device)
         # unsharded: the global stream, exactly as the reference; sharded: a private stream
-        self._rng = random if world == 1 else random.Random(0x9E3779B9 * (rank + 1) + world)
+        if world == 1:
+            self._rng = random
+        else:
+            digest = hashlib.sha256(repr(random.getstate()).encode()).digest()
+            self._rng = random.Random(int.from_bytes(digest[:8], "little") * 1_000_003 + rank * 1009 + world)
 
     def __len__(self):
         return self.states.shape[0]
@@ -54,6 +62,19 @@ class SamplePool:
         idx = self._rng.sample(range(len(self)), batch_size)
         sel = torch.as_tensor(idx, dtype=torch.long, device=self.states.device)
         return idx, self.states.index_select(0, sel)
+
+    def rng_state(self):
+        """The private slot-index stream's state (a sharded pool), else None (the global stream is
+        the caller's to save).  JSON/torch.save-friendly (nested lists)."""
+        if self._rng is random:
+            return None
+        v, st, g = self._rng.getstate()
+        return [v, list(st), g]
+
+    def set_rng_state(self, state):
+        if state is not None and self._rng is not random:
+            v, st, g = state
+            self._rng.setstate((int(v), tuple(int(t) for t in st), g))
 
     def replace(self, idx, new_samples):
         """Write ``new_samples`` (detached) into slots ``idx`` (pool.py:34-42)."""

@@ -66,34 +66,42 @@ def make_desc(*, B, C, H, W, hidden, d_model, offsets, flags, update_gain, alpha
 _WCACHE: dict = {}
 
 
+def _dev_index(device) -> int:
+    device = torch.device(device)
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
 def make_weights(tensors: dict) -> tuple[L.Weights, list]:
     """tensors: name -> device tensor (reference layouts).  Returns the struct and the list of
     contiguous tensors that must stay alive until the launch is enqueued.
 
-    Cached by the tensors' storage addresses when every tensor is already a contiguous float32
-    device tensor (then the struct points at the tensors themselves, which the cache keeps alive,
-    so an address cannot be reused by another tensor; in-place updates such as optimiser steps
-    keep the addresses and need no rebuild).  Building the struct was ~20 us of host time per
-    step at the trainer's size."""
-    key = tuple((name, t.data_ptr()) for name, t in tensors.items() if t is not None)
+    When every tensor is already a contiguous float32 device tensor the struct holds exactly their
+    addresses, so it is cached by (device, name, address): a hit rebuilds nothing (in-place updates
+    such as optimiser steps keep the addresses), and because the struct is a pure function of the
+    key the cache holds no tensor references (the weights of a deleted model are freed; a later
+    tensor at the same address gets the same, correct struct).  Building the struct was ~20 us of
+    host time per step at the trainer's size."""
+    key = tuple((name, t.device.index, t.data_ptr()) for name, t in tensors.items() if t is not None)
+    keep = [t for t in tensors.values() if t is not None]
     hit = _WCACHE.get(key)
     if hit is not None:
-        return hit
+        return hit, keep
     w = L.Weights()
-    keep = []
     cacheable = True
+    conv = []
     for name, t in tensors.items():
         if t is None:
             continue
         cacheable &= t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
         t = _dev_f32(t.detach(), name)
-        keep.append(t)
+        conv.append(t)
         setattr(w, name, t.data_ptr())
     if cacheable:
-        if len(_WCACHE) >= 64:
+        if len(_WCACHE) >= 256:
             _WCACHE.clear()
-        _WCACHE[key] = (w, keep)
-    return w, keep
+        _WCACHE[key] = w
+        return w, keep
+    return w, conv
 
 
 _WS_BYTES: dict = {}
@@ -103,7 +111,8 @@ def workspace(desc: L.StepDesc, device) -> torch.Tensor:
     # the size depends on the shape class and the offsets' radius (the tile plan), not on the
     # offsets themselves or the knobs' values
     o = desc.offsets[:2 * desc.num_offsets]
-    key = (desc.B, desc.C, desc.H, desc.W, desc.hidden, desc.d_model, desc.num_offsets, desc.flags,
+    # (the plan also depends on the device's CU count: keyed by device)
+    key = (_dev_index(device), desc.B, desc.C, desc.H, desc.W, desc.hidden, desc.d_model, desc.num_offsets, desc.flags,
            desc.message_gain != 0.0, desc.fire_mode,
            max((abs(v) for v in o[0::2]), default=0), max((abs(v) for v in o[1::2]), default=0))
     n = _WS_BYTES.get(key)

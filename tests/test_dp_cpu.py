@@ -18,8 +18,8 @@ from tests.grad_helpers import premult_loss_and_grad
 B, H = 4, 12
 
 
-def _setup():
-    c = Case("grad_graph_zeropad_latest_grown_b2_40")
+def _setup(fixture="grad_graph_zeropad_latest_grown_b2_40"):
+    c = Case(fixture)
     p = {k: v.astype(np.float64) for k, v in c.weights.items()}
     rng = np.random.default_rng(1)
     x = rng.random((B, 16, H, H))
@@ -29,10 +29,10 @@ def _setup():
     return c, p, x, fire, target
 
 
-def _grads(lo, hi):
+def _grads(lo, hi, fixture="grad_graph_zeropad_latest_grown_b2_40"):
     """Gradients of the mean premultiplied-RGBA loss over samples [lo, hi)."""
-    c, p, x, fire, target = _setup()
-    chosen = c.chosen(0)
+    c, p, x, fire, target = _setup(fixture)
+    chosen = c.chosen(0) if c.meta["graph"] else None
     out = O.nca_step(x[lo:hi], p, c.cfg(), chosen=chosen, fire_mask=fire[lo:hi])
     _, g = premult_loss_and_grad(out, target)
     _, grads = V.nca_step_vjp(x[lo:hi], p, c.cfg(), g, chosen=chosen, fire_mask=fire[lo:hi])
@@ -48,31 +48,64 @@ def _params(grads):
     return ps
 
 
-def _worker(rank, world, port, q):
-    from graph_neural_cellular_automata_amd.dp import allreduce_gradients, normalize_gradients_
+def _worker(rank, world, port, q, fixture=None, policy="normalize"):
+    from graph_neural_cellular_automata_amd.dp import POLICIES, allreduce_gradients, clip_gradients_
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     half = B // world
-    ps = _params(_grads(rank * half, (rank + 1) * half))
+    ps = _params(_grads(rank * half, (rank + 1) * half, *([fixture] if fixture else [])))
     nbytes = allreduce_gradients(ps)
     avg = [p.grad.clone().numpy() for p in ps]
-    normalize_gradients_(ps)
+    if policy.startswith("clip:"):   # the classic trainer's clip at a max norm this case exceeds
+        clip_gradients_(ps, float(policy[5:]))
+    else:
+        POLICIES[policy](ps)
     if rank == 0:
         q.put((nbytes, avg, [p.grad.numpy() for p in ps]))
     dist.destroy_process_group()
 
 
-def test_two_rank_allreduce_equals_full_batch():
+def _run_two_ranks(fixture=None, policy="normalize"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29700 + (os.getpid() % 1000)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    port = 29700 + (os.getpid() % 1000) + (7 if policy != "normalize" else 0)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, fixture, policy)) for r in range(2)]
     for pr in procs:
         pr.start()
-    nbytes, avg, normed = q.get(timeout=120)
+    res = q.get(timeout=120)
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
+    return res
+
+
+def test_two_rank_allreduce_then_clip_equals_full_batch():
+    """The classic trainer's policy (train_intermediate_loss.py:282, clip_grad_norm_) after the
+    all-reduce: equals clipping the single-process full-batch gradient (the global norm is not
+    linear in the per-rank gradients, so the clip must follow the all-reduce).  This small case's
+    gradient norm is ~0.009, so it clips at 0.004 (the trainer's 0.5 would leave it unchanged)."""
+    fx, max_norm = "grad_classic_ep980_b2_32", 0.004
+    nbytes, avg, clipped = _run_two_ranks(fx, f"clip:{max_norm}")
+    full = _grads(0, B, fx)
+    keys = sorted(full)
+    total = np.sqrt(sum(float((full[k] ** 2).sum()) for k in keys))
+    coef = min(1.0, max_norm / (total + 1e-6))
+    assert total > max_norm   # the case exercises the clip
+    for k, a, c in zip(keys, avg, clipped):
+        np.testing.assert_allclose(a, full[k], rtol=1e-12, atol=1e-15)
+        np.testing.assert_allclose(c, full[k] * coef, rtol=1e-10, atol=1e-15)
+    # clipping each rank's gradient before averaging gives a different answer
+    halves = [_grads(0, B // 2, fx), _grads(B // 2, B, fx)]
+    pre = []
+    for h in halves:
+        n = np.sqrt(sum(float((h[k] ** 2).sum()) for k in keys))
+        pre.append({k: h[k] * min(1.0, max_norm / (n + 1e-6)) for k in keys})
+    wrong = {k: 0.5 * (pre[0][k] + pre[1][k]) for k in keys}
+    assert max(np.abs(wrong[k] - full[k] * coef).max() for k in keys) > 1e-6
+
+
+def test_two_rank_allreduce_equals_full_batch():
+    nbytes, avg, normed = _run_two_ranks()
     full = _grads(0, B)
     keys = sorted(full)
     assert nbytes == 8 * sum(full[k].size for k in keys)

@@ -1,0 +1,88 @@
+"""Long-rollout drift of the SHIPPING kernels against the float64 oracle (a 96-step
+rollout within atol 1e-4 and no alive-mask flips).
+
+Each case runs ``gnca_rollout_f32`` at a batch large enough that the planner picks the kernels the
+benchmark runs — the bf16x6 split K1 with the compact update field and the K2 -> K1 alive-byte
+hand-over — asserts that plan (``S.k1_variant`` / ``S.rollout_compact``), and compares a few samples
+with the oracle stepped in float64 on the same offsets and hashed fire masks (global sample index
+``sample_base + i``).  Reference path: ``ncagraph.py:106-168`` (graph), ``nca.py:64-105`` (classic).
+Weights: the reference's trained checkpoints carried by the golden fixtures (graph nca_latest.pt,
+classic nca_epoch980.pt) or, for 32 channels, the fixture's seeded init (W2 ~ N(0, 0.02))."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nca_oracle as O
+from tests.golden_io import Case
+
+pytestmark = pytest.mark.gpu
+
+# case -> (fixture, graph, C, H, B, R, K, steps, samples checked, expected K1)
+CASES = {
+    # the headline's shape class: B=96 x 16 x 72^2 graph torus r=4 K=8 -> 576 tiles of 24x36
+    "graph_split24x36": ("graph_torus_latest_grown_b1_72", True, 16, 72, 96, 4, 8, 96, (0, 47, 95),
+                         "gnca_k1_split<24,36,4,4,8>"),
+    # classic NCA (BASELINE config 2's step) on the classic split K1
+    "classic_split8x24": ("classic_ep980_b2_32", False, 16, 72, 96, 0, 0, 96, (0, 47, 95),
+                          "gnca_k1_split<8,24,1,4,0>"),
+    # BASELINE config 5's shape class: 32 ch, 128^2, r=5, K=16 (48 steps: the f64 oracle's time)
+    "c5_split32": ("graph_torus_c32_r5_k16_b1_48", True, 32, 128, 8, 5, 16, 48, (0, 7),
+                   "gnca_k1_split32<16,16,5,5,16>"),
+}
+GAIN, THR, MSG, FIRE, SEED = 0.05, 0.12, 0.25, 0.5, 5
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    return torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    fx, graph, C, H, B, R, K, T, check, k1_expected = CASES[case]
+    c = Case(fx)
+    p64 = {k: v.astype(np.float64) for k, v in c.weights.items()}
+    wt = {k: torch.from_numpy(np.ascontiguousarray(v.astype(np.float32))).to(dev) for k, v in c.weights.items()}
+    tensors = dict(perception=wt["perception.conv.weight"], w1=wt["update_net.0.weight"],
+                   b1=wt["update_net.0.bias"], w2=wt["update_net.2.weight"],
+                   gn_weight=wt["norm.weight"], gn_bias=wt["norm.bias"])
+    if graph:
+        tensors.update(wq=wt["graph.query_proj.weight"], bq=wt["graph.query_proj.bias"],
+                       wk=wt["graph.key_proj.weight"], bk=wt["graph.key_proj.bias"],
+                       wm=wt["graph.msg_proj.weight"], bm=wt["graph.msg_proj.bias"],
+                       scaling=wt["graph.scaling"])
+    w, keep = S.make_weights(tensors)
+    # the bench's synthetic state: RGB, alpha ~ U(0,1), hidden ~ N(0,1)
+    g = torch.Generator(device=dev).manual_seed(31)
+    x = torch.rand(B, C, H, H, device=dev, generator=g)
+    x[:, 4:] = torch.randn(B, C - 4, H, H, device=dev, generator=g)
+    table = O.build_offsets(R) if graph else []
+    rr = random.Random(17)
+    offs = [rr.sample(table, K) if graph else [] for _ in range(T)]
+    flags = L.USE_GROUPNORM | ((L.GRAPH | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE) if graph else 0)
+    base = 1000
+    d = S.make_desc(B=B, C=C, H=H, W=H, hidden=128, d_model=16, offsets=offs[0], flags=flags,
+                    update_gain=GAIN, alpha_thr=THR, message_gain=MSG, fire_rate=FIRE,
+                    fire_mode=L.FIRE_HASH, rng_seed=SEED, rng_step=0, sample_base=base)
+    name, arith = S.k1_variant(d)
+    assert (name, arith) == (k1_expected, "bf16x6")
+    assert S.rollout_compact(d), "the rollout must run on the compact update field"
+    got = S.rollout(d, w, x.contiguous(), T, offs).cpu().numpy()
+    assert np.isfinite(got).all()
+    cfg = dict(update_gain=GAIN, alpha_thr=THR, use_groupnorm=True, graph=graph, message_gain=MSG,
+               hidden_only=True, zero_padded_shift=False, alive_to_alive=True)
+    idx = np.array(check)
+    ref = x.cpu().numpy()[idx].astype(np.float64)
+    for t in range(T):
+        fm = np.concatenate([O.hash_fire_mask(SEED, t, base + int(i), 1, H, H, FIRE) for i in idx])
+        ref = O.nca_step(ref, p64, cfg, chosen=offs[t] if graph else None, fire_mask=fm)
+    err = np.abs(got[idx] - ref).max()
+    print(f"[drift] {case}: {name}, {T} steps, samples {list(check)}: max |hip - f64| = {err:.3e}")
+    assert err <= 1e-4, err
+    np.testing.assert_array_equal(O.alive_mask(got[idx], THR), O.alive_mask(ref, THR))

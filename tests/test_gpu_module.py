@@ -337,11 +337,11 @@ def test_large_batch_path_vs_oracle(dev, graph):
 
 
 @pytest.mark.parametrize("msg", [0.25, 0.0])
-def test_c32_two_phase_path_vs_oracle(dev, msg):
+def test_c32_split32_path_vs_oracle(dev, msg):
     """BASELINE config 5's shape class (32 ch, 128 x 128, r = 5, K = 16) at B=64 takes the
-    two-channel-phase K1 (gnca_k1_2ph): two samples of one step against the float64 oracle
-    (message on, and message_gain 0 = the classic-style no-gather variant), and a shard split is
-    bitwise equal."""
+    32-channel split K1 (gnca_k1_split32, channels staged in two 16-channel phases): two samples
+    of one step against the float64 oracle (message on, and message_gain 0 = the no-gather
+    variant), and a shard split is bitwise equal."""
     from graph_neural_cellular_automata_amd import NeuralCAGraph
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
@@ -366,6 +366,8 @@ def test_c32_two_phase_path_vs_oracle(dev, msg):
                            update_gain=0.05, alpha_thr=0.12, message_gain=msg, fire_rate=0.5,
                            fire_mode=L.FIRE_HASH, rng_seed=42, rng_step=1, sample_base=base)
 
+    name, arith = S.k1_variant(desc(B, 0))
+    assert arith == "bf16x6" and name.startswith("gnca_k1_split32<16,16,"), name
     out, _ = S.step(desc(B, 0), w, x)
     p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
     cfg = dict(update_gain=0.05, alpha_thr=0.12, use_groupnorm=True, graph=True,

@@ -75,3 +75,35 @@ def test_sharded_pool_sampling_keeps_global_stream():
         assert batch.shape[0] == 3
         after.append(random.random())
     assert after[0] == after[1] == after[2]
+
+
+def test_sharded_pool_stream_follows_user_seed_and_checkpoints(tmp_path):
+    """The private slot-index stream of a sharded pool depends on the user's random.seed (read from
+    the global state, not consumed), differs per rank, and survives a checkpoint round trip."""
+    import torch.nn as nn
+
+    from graph_neural_cellular_automata_amd.checkpoint import load_checkpoint, save_checkpoint
+
+    def draws(seed, rank):
+        random.seed(seed)
+        p = SamplePool(12, _seed_fn, shard=(rank, 2))
+        after = random.random()
+        return [p.sample(3)[0] for _ in range(4)], after, p
+
+    a, after_a, _ = draws(1, 0)
+    b, after_b, _ = draws(2, 0)
+    c, _, _ = draws(1, 1)
+    random.seed(1)
+    assert after_a == random.random()   # building the sharded pool consumed nothing
+    assert a != b and a != c
+    # checkpoint: resume continues the sequence
+    _, _, p = draws(7, 1)
+    p.sample(3)
+    model = nn.Linear(2, 2)
+    opt = torch.optim.Adam(model.parameters())
+    save_checkpoint(str(tmp_path), "epoch1", model, opt, None, 1, 10, pool=p)
+    expect = [p.sample(3)[0] for _ in range(3)]
+    _, _, q = draws(99, 1)
+    payload = torch.load(str(tmp_path / "nca_epoch1.pt"), weights_only=True)
+    load_checkpoint(payload, model, opt, None, pool=q)
+    assert [q.sample(3)[0] for _ in range(3)] == expect
