@@ -594,26 +594,40 @@ def main():
         raise SystemExit(f"bench: the launch-by-launch replay differs from the timed rollout: "
                          f"{int(diff.sum())} values, max |d| {float((src - out).abs().nan_to_num().max()):.3e}, "
                          f"NaN {int(src.isnan().sum())}/{int(out.isnan().sum())}")
-    # --- per-kernel durations: a second replay with ONLY the K1/K2 launches on the stream and a
-    #     HIP event between consecutive launches (no torch kernels in between) ---
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps + 1)]
-    src = start
+    # --- per-kernel durations of the timed rollout itself: the same rollout again (same start state,
+    #     offsets and fire counters; final state checked bitwise) through gnca_rollout_stamped_f32,
+    #     where every K1 / K2 workgroup writes wall-clock stamps (100 MHz s_memrealtime) at its start
+    #     and end: a launch's duration is max(end) - min(start), with nothing inserted in the stream
+    #     between launches.  The stamped run's own wall time is reported beside the timed one. ---
+    cap = 16384
+    stamps = torch.zeros(args.steps * 4 * cap, dtype=torch.int64, device=dev)
+    arr = (ctypes.c_int8 * len(timed_offsets))(*timed_offsets) if timed_offsets else None
+    d = make_desc(wl, B, H, H, offsets_table[:K], rank, args.warmup)
+    dst2 = torch.empty_like(x)
     torch.cuda.synchronize()
-    evs[0].record(stream)
+    t_s = time.perf_counter()
+    L.check(lib.gnca_rollout_stamped_f32(ctypes.byref(d), ctypes.byref(w), args.steps, arr, start.data_ptr(),
+                                         dst2.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(),
+                                         stamps.data_ptr(), cap, sptr), "gnca_rollout_stamped_f32")
+    torch.cuda.synchronize()
+    stamped_ms = (time.perf_counter() - t_s) * 1e3 / args.steps
+    if not torch.equal(dst2.view(torch.int32), out.view(torch.int32)):
+        raise SystemExit("bench: the stamped rollout differs from the timed rollout")
+    sv = stamps.view(args.steps, 2, cap, 2).cpu().numpy()
+    dur = np.zeros((args.steps, 2))
+    first, last = None, None
     for t in range(args.steps):
-        dst = bufs[t % 2]
-        launch(t, src, dst, 1)
-        evs[2 * t + 1].record(stream)
-        launch(t, src, dst, 2)
-        evs[2 * t + 2].record(stream)
-        src = dst
-    torch.cuda.synchronize()
-    if not torch.equal(src.view(torch.int32), out.view(torch.int32)):
-        raise SystemExit("bench: the timing replay differs from the timed rollout")
-    k1_all = [evs[2 * t].elapsed_time(evs[2 * t + 1]) for t in range(args.steps)]
-    k2_all = [evs[2 * t + 1].elapsed_time(evs[2 * t + 2]) for t in range(args.steps)]
-    k1_ms = sum(k1_all) / len(k1_all)
-    k2_ms = sum(k2_all) / len(k2_all)
+        for k in range(2):
+            used = sv[t, k, :, 0] > 0
+            if not used.any():
+                raise SystemExit(f"bench: no stamps from step {t} kernel {k}")
+            t0_, t1_ = int(sv[t, k, used, 0].min()), int(sv[t, k, used, 1].max())
+            dur[t, k] = (t1_ - t0_) * 1e-5          # 100 MHz ticks -> ms
+            first = t0_ if first is None else min(first, t0_)
+            last = t1_ if last is None else max(last, t1_)
+    k1_ms, k2_ms = float(dur[:, 0].mean()), float(dur[:, 1].mean())
+    span_ms = (last - first) * 1e-5 / args.steps
+    del stamps, dst2
     launches = args.steps
     live_frac = float(live) / (cells * launches)
     fpc = flop_per_cell(wl)
@@ -653,8 +667,9 @@ def main():
             "traffic": pmc_traffic("K1") if headline else None,
             "traffic_unit": f"bytes/launch (2*FETCH_SIZE+WRITE_SIZE, {os.path.relpath(PMC_TRAFFIC, ROOT)})",
             "k1_ms": k1_ms,
-            "k1_ms_source": "HIP events on the launch stream between consecutive launches of a replay "
-                            "of the timed rollout holding only its K1/K2 launches",
+            "k1_ms_source": "per-workgroup s_memrealtime stamps (first instruction .. after the last "
+                            "barrier, max - min over the launch's workgroups) in an identical re-run of "
+                            "the timed rollout (gnca_rollout_stamped_f32; final state bitwise equal)",
             "mfma_pipe_frac_est": exec_flops / k1_s / peak_dtype,
             "mfma_pipe_note": "executed MFMA FLOPs in the MFMA's dtype (32-cell groups, padding "
                               "included) / that dtype's dense peak",
@@ -690,6 +705,10 @@ def main():
             "ranks_seen": ranks_seen, "backend": (args.dist_backend if world > 1 else None),
             "rank_state_checksums": rank_sums,
             "k1_k2_ms_vs_step": (k1_ms + k2_ms) / ms,
+            "device_timeline": {"stamped_rollout_ms_per_step": stamped_ms,
+                                "first_k1_start_to_last_k2_end_ms_per_step": span_ms,
+                                "k1_ms": k1_ms, "k2_ms": k2_ms,
+                                "gaps_ms_per_step": span_ms - k1_ms - k2_ms},
             "roofline": roof, "roofline_k2": roof_k2, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -25,6 +25,14 @@ constexpr int kThreads = 256;
 #define GNCA_AB_ENV(name) ((const char*)nullptr)
 #endif
 
+// Measurement (gnca_rollout_stamped_f32): per-workgroup wall-clock stamps from the 100 MHz
+// s_memrealtime counter, st[2 * blockIdx.x + which] (0 = first instruction, 1 = after the
+// workgroup's last barrier).  st == NULL (every product launch): one uniform branch, no store.
+__device__ __forceinline__ void wg_stamp(uint64_t* st, int which) {
+  if (st != nullptr && threadIdx.x == 0) st[2 * blockIdx.x + which] = __builtin_amdgcn_s_memrealtime();
+}
+#define GNCA_STAMP_END(st) do { if ((st) != nullptr) { __syncthreads(); wg_stamp((st), 1); } } while (0)
+
 __device__ __forceinline__ int wrapi(int v, int n) {
   v %= n;
   return v < 0 ? v + n : v;

@@ -163,6 +163,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
   constexpr int NG = (TH * TW + 31) / 32;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  wg_stamp(a.stamps, 0);
   const int h = lane >> 5, r32 = lane & 31, c16 = lane & 15;
   const int H = a.H, W = a.W;
   const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
@@ -664,6 +665,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
     par ^= 1;
   }
   PROF_STORE_W03;
+  GNCA_STAMP_END(a.stamps);
 }
 
 }  // namespace gnca

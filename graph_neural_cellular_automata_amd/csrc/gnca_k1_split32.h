@@ -71,6 +71,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   constexpr bool GRAPH = KU > 0;
   constexpr int PW = NW - 1;   // the preparer / next-tile stager (no group unless > 224 live cells)
 
+  wg_stamp(a.stamps, 0);
   float* xs = reinterpret_cast<float*>(smem_b + L.xs);
   int* cnt = reinterpret_cast<int*>(smem_b + L.cnt);
   int* xsd = cnt + 2;   // groups past their phase-1 reads, 64 per group (monotonic over the tiles)
@@ -524,6 +525,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     tile = nxt;
     par ^= 1;
   }
+  GNCA_STAMP_END(a.stamps);
 }
 
 }  // namespace gnca

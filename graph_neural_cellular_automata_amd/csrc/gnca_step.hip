@@ -166,6 +166,7 @@ struct K1Args {
   int B, C, H, W, hidden, k, RY, RX, TH, TW, tiles_x, tps, total_tiles, fire_mode;
   float fire_rate, alpha_thr, graph_alpha_thr, message_gain, uniform_w;
   uint32_t flags;
+  uint64_t* stamps;    // measurement only (null in product launches): per-workgroup wall-clock stamps
   int odl[GNCA_MAX_OFFSETS];   // gather source delta in the staged region: dy*RW + dx (pad: dy*RW)
 };
 
@@ -190,6 +191,7 @@ namespace gnca {
 template <int CP, int HDP, int TH_, int TW_, int RY_, int RX_, int KU_, int NT = kThreads>
 __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  wg_stamp(a.stamps, 0);
   constexpr int CPQ = CP / 4, KS = 3 * CPQ, MT = HDP / 16, MO = (CP + 15) / 16;
   constexpr int KSP = ((((KS + 3) & ~3) >> 2) & 1) ? ((KS + 3) & ~3) : ((KS + 3) & ~3) + 4;
   constexpr int S2r = 4 * MT;
@@ -838,6 +840,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void gnca_k1_update(const K1Args a) {
     PROF_MARK(5);   // per-tile reduction
   }
   PROF_STORE;
+  GNCA_STAMP_END(a.stamps);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -864,6 +867,7 @@ struct K2Args {
   const uint32_t* rpre;
   const float* dxa;        // [B,H,W] alpha-channel update of the live cells (K1Args::dxa)
   int TH, TW, tiles_x;
+  uint64_t* stamps;        // measurement only (K1Args::stamps)
 };
 
 // K2's sample for block-row j.  zigzag: K1 sweeps 8 contiguous sample ranges (one per XCD group)
@@ -1126,6 +1130,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float sh_norm[4 + 64];
   const int tid = threadIdx.x;
+  wg_stamp(a.stamps, 0);
   const int bj = blockIdx.x / a.nbands, band = blockIdx.x - bj * a.nbands;
   const int b = k2_sample(bj, a.B, a.zigzag);
   if (a.active && !a.active[b]) {   // masked step: an inactive sample passes through unchanged
@@ -1138,9 +1143,11 @@ __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
       const int c = it / nbc, e = it - c * nbc;
       os_[(size_t)c * HW + (size_t)r0 * a.W + e] = xs_[(size_t)c * HW + (size_t)r0 * a.W + e];
     }
+    GNCA_STAMP_END(a.stamps);
     return;
   }
   k2_body<V, COMPACT>(a, smem, sh_norm);
+  GNCA_STAMP_END(a.stamps);
 }
 
 // This step's pre-update masks as bytes for the split K1 when no previous K2 handed them over
@@ -1672,7 +1679,8 @@ static bool weights_ok(const gnca_step_desc* d, const gnca_weights* w, bool msg_
 static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float* x, float* x_out,
                      const void* fire, float* attn, void* ws, size_t ws_bytes, hipStream_t st,
                      uint32_t phases = GNCA_PHASE_ALL, const uint8_t* active = nullptr,
-                     bool alive_in = false, bool alive_out = false, bool compact = false) {
+                     bool alive_in = false, bool alive_out = false, bool compact = false,
+                     uint64_t* stamps = nullptr, int stamp_cap = 0) {
   Plan P;
   if (!make_plan(d, false, &P)) {
     if (d && d->C >= 4 && d->hidden > 0 && !find_variant(d->C, d->hidden)) return GNCA_ERR_UNSUPPORTED;
@@ -1720,6 +1728,11 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
     k1.rpre = rpre;
     k1.dxa = dxa;
   }
+  // measurement: K1's workgroups stamp into stamps[0 .. 2*cap), K2's into stamps[2*cap .. 4*cap)
+  k1.stamps = stamps;
+  if (stamps && (long)std::min<long>((long)device_cus() * occupancy(P.var->fn, P.lds1, P.var->NT),
+                                     P.total_tiles) > stamp_cap)
+    return GNCA_ERR_INVALID;
   if ((phases & GNCA_PHASE_K1) && (rc = launch_k1(k1, P, st)) != GNCA_OK) return rc;
   if (!(phases & GNCA_PHASE_K2)) return GNCA_OK;
   K2Args k2;
@@ -1749,6 +1762,10 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
     k2.TH = P.TH;
     k2.TW = P.TW;
     k2.tiles_x = P.tiles_x;
+  }
+  if (stamps) {
+    if ((compact ? P.total2_c : P.total2) > stamp_cap) return GNCA_ERR_INVALID;
+    k2.stamps = stamps + 2 * (size_t)stamp_cap;
   }
   auto k2fn = compact ? ((d->W & 3) == 0 ? gnca_k2_finalize<4, true> : gnca_k2_finalize<1, true>)
                       : ((d->W & 3) == 0 ? gnca_k2_finalize<4, false> : gnca_k2_finalize<1, false>);
@@ -1894,9 +1911,11 @@ int gnca_fire_mask_u8(const gnca_step_desc* desc, uint8_t* mask, void* stream) {
   return check_launch();
 }
 
-int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
-                     const int8_t* offsets, const float* x, float* x_final, float* scratch,
-                     void* ws, size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
+                        const int8_t* offsets, const float* x, float* x_final, float* scratch,
+                        void* ws, size_t ws_bytes, void* stream, uint64_t* stamps, int stamp_cap) {
   if (!desc || steps < 0 || !x || !x_final || !scratch) return GNCA_ERR_INVALID;
   if (desc->fire_mode != GNCA_FIRE_NONE && desc->fire_mode != GNCA_FIRE_HASH) return GNCA_ERR_INVALID;
   if (x == x_final || x == scratch || x_final == scratch) return GNCA_ERR_INVALID;
@@ -1918,11 +1937,29 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
     dt.rng_step = desc->rng_step + t;
     if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(dt.offsets, offsets + (size_t)t * 2 * k, 2 * k);
     const int rc = step_impl(&dt, w, src, dst, nullptr, nullptr, ws, ws_bytes, st, GNCA_PHASE_ALL,
-                             nullptr, hand_alive && t > 0, hand_alive && t + 1 < steps, true);
+                             nullptr, hand_alive && t > 0, hand_alive && t + 1 < steps, true,
+                             stamps ? stamps + (size_t)t * 4 * stamp_cap : nullptr, stamp_cap);
     if (rc != GNCA_OK) return rc;
     src = dst;
   }
   return GNCA_OK;
+}
+
+extern "C" {
+
+int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
+                     const int8_t* offsets, const float* x, float* x_final, float* scratch,
+                     void* ws, size_t ws_bytes, void* stream) {
+  return rollout_impl(desc, w, steps, offsets, x, x_final, scratch, ws, ws_bytes, stream, nullptr, 0);
+}
+
+int gnca_rollout_stamped_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
+                             const int8_t* offsets, const float* x, float* x_final, float* scratch,
+                             void* ws, size_t ws_bytes, uint64_t* stamps, int32_t stamp_cap,
+                             void* stream) {
+  if (!stamps || stamp_cap <= 0) return GNCA_ERR_INVALID;
+  return rollout_impl(desc, w, steps, offsets, x, x_final, scratch, ws, ws_bytes, stream, stamps,
+                      stamp_cap);
 }
 
 }  // extern "C"

@@ -186,6 +186,19 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
                      void* ws, size_t ws_bytes, void* stream);
 
 /*
+ * Measurement twin of gnca_rollout_f32: the same launches, and every K1 / K2 workgroup also writes
+ * two wall-clock stamps (the 100 MHz s_memrealtime counter: at its first instruction and after its
+ * last barrier) into `stamps` (device memory, uint64, zero-initialised by the caller):
+ *   stamps[((t * 2 + k) * stamp_cap + wg) * 2 + {0: start, 1: end}],  t = step, k = 0 (K1) / 1 (K2)
+ * so a launch's duration is max(end) - min(start) over its workgroups, with no event or marker in
+ * the stream between launches.  GNCA_ERR_INVALID if a launch has more than stamp_cap workgroups.
+ */
+int gnca_rollout_stamped_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
+                             const int8_t* offsets, const float* x, float* x_final, float* scratch,
+                             void* ws, size_t ws_bytes, uint64_t* stamps, int32_t stamp_cap,
+                             void* stream);
+
+/*
  * The fire mask a GNCA_FIRE_HASH step would draw: mask[b,0,i,j] = u(rng_seed, rng_step,
  * sample_base+b, i*W+j) <= fire_rate, as uint8 [B,1,H,W] (1 = fires).  For inspection and for
  * replaying a hash-masked rollout elsewhere (e.g. as GNCA_FIRE_MASK_U8).
