@@ -38,6 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HD, D_MODEL = 128, 16
+PIECE = 8   # rollout steps per host call (the next piece's offsets are drawn while this one runs)
 GAIN, THR, MSG_GAIN, FIRE = 0.05, 0.12, 0.25, 0.5
 PEAK_F32_MFMA = 157.3e12                               # MI355X_MICROARCH.md, FP32 matrix
 PEAK_BF16_MFMA = 2.5e15                                # MI355X_MICROARCH.md, BF16 dense
@@ -487,19 +488,32 @@ def main():
 
     rr = random.Random(42)  # same seed on every rank: identical offsets, no communication
 
+    tmp = torch.empty_like(x)
+
     def rollout(n, step0, src, dst, record=None, rng=rr):
-        flat = []
-        if graph:
-            for _ in range(n):   # the per-step host draw (graph_augmentation.py:121), timed
-                for dy, dx in rng.sample(offsets_table, K):
-                    flat += [dy, dx]
-        if record is not None:
-            record.extend(flat)
-        arr = (ctypes.c_int8 * len(flat))(*flat) if flat else None
-        d = make_desc(wl, B, H, H, offsets_table[:K], rank, step0)
-        rc = lib.gnca_rollout_f32(ctypes.byref(d), ctypes.byref(w), n, arr, src.data_ptr(),
-                                  dst.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(), sptr)
-        L.check(rc, "gnca_rollout_f32")
+        """n steps from src into dst, issued in pieces of PIECE steps (gnca_rollout_ex_f32 with the
+        alive masks handed over between pieces: bitwise the one-call rollout): the host draws the
+        next piece's offsets (graph_augmentation.py:121, timed) while the device runs this one."""
+        npieces = (n + PIECE - 1) // PIECE
+        cur = src
+        for p in range(npieces):
+            m = min(PIECE, n - p * PIECE)
+            flat = []
+            if graph:
+                for _ in range(m):
+                    for dy, dx in rng.sample(offsets_table, K):
+                        flat += [dy, dx]
+            if record is not None:
+                record.extend(flat)
+            arr = (ctypes.c_int8 * len(flat))(*flat) if flat else None
+            d = make_desc(wl, B, H, H, offsets_table[:K], rank, step0 + p * PIECE)
+            nxt = dst if (npieces - 1 - p) % 2 == 0 else tmp
+            fl = (L.ROLLOUT_ALIVE_IN if p > 0 else 0) | (L.ROLLOUT_ALIVE_OUT if p + 1 < npieces else 0)
+            rc = lib.gnca_rollout_ex_f32(ctypes.byref(d), ctypes.byref(w), m, arr, cur.data_ptr(),
+                                         nxt.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(),
+                                         fl, sptr)
+            L.check(rc, "gnca_rollout_ex_f32")
+            cur = nxt
 
     # warmup: the rollout's first W steps, untimed; the K timed steps continue from their state (and
     # fire counters), as one rollout of W + K steps
@@ -548,6 +562,40 @@ def main():
     cells = B * H * H
     value = cells * args.steps * world / el
 
+    # --- per-kernel durations of the timed rollout itself: the same rollout again (same start state,
+    #     offsets and fire counters; final state checked bitwise) through gnca_rollout_stamped_f32,
+    #     where every K1 / K2 workgroup writes wall-clock stamps (100 MHz s_memrealtime) at its start
+    #     and end: a launch's duration is max(end) - min(start), with nothing inserted in the stream
+    #     between launches.  The stamped run's own wall time is reported beside the timed one. ---
+    cap = 16384
+    stamps = torch.zeros(args.steps * 4 * cap, dtype=torch.int64, device=dev)
+    arr = (ctypes.c_int8 * len(timed_offsets))(*timed_offsets) if timed_offsets else None
+    d = make_desc(wl, B, H, H, offsets_table[:K], rank, args.warmup)
+    dst2 = torch.empty_like(x)
+    torch.cuda.synchronize()
+    t_s = time.perf_counter()
+    L.check(lib.gnca_rollout_stamped_f32(ctypes.byref(d), ctypes.byref(w), args.steps, arr, start.data_ptr(),
+                                         dst2.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(),
+                                         stamps.data_ptr(), cap, sptr), "gnca_rollout_stamped_f32")
+    torch.cuda.synchronize()
+    stamped_ms = (time.perf_counter() - t_s) * 1e3 / args.steps
+    if not torch.equal(dst2.view(torch.int32), out.view(torch.int32)):
+        raise SystemExit("bench: the stamped rollout differs from the timed rollout")
+    sv = stamps.view(args.steps, 2, cap, 2).cpu().numpy()
+    dur = np.zeros((args.steps, 2))
+    first, last = None, None
+    for t in range(args.steps):
+        for k in range(2):
+            used = sv[t, k, :, 0] > 0
+            if not used.any():
+                raise SystemExit(f"bench: no stamps from step {t} kernel {k}")
+            t0_, t1_ = int(sv[t, k, used, 0].min()), int(sv[t, k, used, 1].max())
+            dur[t, k] = (t1_ - t0_) * 1e-5          # 100 MHz ticks -> ms
+            first = t0_ if first is None else min(first, t0_)
+            last = t1_ if last is None else max(last, t1_)
+    k1_ms, k2_ms = float(dur[:, 0].mean()), float(dur[:, 1].mean())
+    span_ms = (last - first) * 1e-5 / args.steps
+    del stamps, dst2
     # --- what K1 executes per launch: replay the timed rollout launch by launch (same start state,
     #     offsets and fire counters; the final state is checked bitwise against the timed one) and
     #     count each launch's live cells (keep = pre-alive AND fire: K1 runs the MLP only for them,
@@ -594,40 +642,6 @@ def main():
         raise SystemExit(f"bench: the launch-by-launch replay differs from the timed rollout: "
                          f"{int(diff.sum())} values, max |d| {float((src - out).abs().nan_to_num().max()):.3e}, "
                          f"NaN {int(src.isnan().sum())}/{int(out.isnan().sum())}")
-    # --- per-kernel durations of the timed rollout itself: the same rollout again (same start state,
-    #     offsets and fire counters; final state checked bitwise) through gnca_rollout_stamped_f32,
-    #     where every K1 / K2 workgroup writes wall-clock stamps (100 MHz s_memrealtime) at its start
-    #     and end: a launch's duration is max(end) - min(start), with nothing inserted in the stream
-    #     between launches.  The stamped run's own wall time is reported beside the timed one. ---
-    cap = 16384
-    stamps = torch.zeros(args.steps * 4 * cap, dtype=torch.int64, device=dev)
-    arr = (ctypes.c_int8 * len(timed_offsets))(*timed_offsets) if timed_offsets else None
-    d = make_desc(wl, B, H, H, offsets_table[:K], rank, args.warmup)
-    dst2 = torch.empty_like(x)
-    torch.cuda.synchronize()
-    t_s = time.perf_counter()
-    L.check(lib.gnca_rollout_stamped_f32(ctypes.byref(d), ctypes.byref(w), args.steps, arr, start.data_ptr(),
-                                         dst2.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(),
-                                         stamps.data_ptr(), cap, sptr), "gnca_rollout_stamped_f32")
-    torch.cuda.synchronize()
-    stamped_ms = (time.perf_counter() - t_s) * 1e3 / args.steps
-    if not torch.equal(dst2.view(torch.int32), out.view(torch.int32)):
-        raise SystemExit("bench: the stamped rollout differs from the timed rollout")
-    sv = stamps.view(args.steps, 2, cap, 2).cpu().numpy()
-    dur = np.zeros((args.steps, 2))
-    first, last = None, None
-    for t in range(args.steps):
-        for k in range(2):
-            used = sv[t, k, :, 0] > 0
-            if not used.any():
-                raise SystemExit(f"bench: no stamps from step {t} kernel {k}")
-            t0_, t1_ = int(sv[t, k, used, 0].min()), int(sv[t, k, used, 1].max())
-            dur[t, k] = (t1_ - t0_) * 1e-5          # 100 MHz ticks -> ms
-            first = t0_ if first is None else min(first, t0_)
-            last = t1_ if last is None else max(last, t1_)
-    k1_ms, k2_ms = float(dur[:, 0].mean()), float(dur[:, 1].mean())
-    span_ms = (last - first) * 1e-5 / args.steps
-    del stamps, dst2
     launches = args.steps
     live_frac = float(live) / (cells * launches)
     fpc = flop_per_cell(wl)

@@ -72,11 +72,13 @@ EXPORTS = ("gnca_abi_version", "gnca_status_string", "gnca_last_hip_error",
            "gnca_workspace_bytes", "gnca_step_f32", "gnca_step_phases_f32", "gnca_message_f32",
            "gnca_perceive_f32", "gnca_rollout_f32", "gnca_bwd_workspace_bytes", "gnca_step_bwd_f32",
            "gnca_fire_mask_u8", "gnca_step_masked_f32", "gnca_damage_f32", "gnca_loss_premult_f32",
-           "gnca_loss_premult_bwd_f32", "gnca_k1_variant", "gnca_rollout_stamped_f32")
+           "gnca_loss_premult_bwd_f32", "gnca_k1_variant", "gnca_rollout_stamped_f32",
+           "gnca_rollout_ex_f32")
 
 PHASE_K0, PHASE_K1, PHASE_K2 = 1, 2, 4
 PHASE_ALL = 7
 PHASE_ALIVE = 8   # rollout mode: K2 hands the next step's alive masks to K1 (include/gnca.h)
+ROLLOUT_ALIVE_IN, ROLLOUT_ALIVE_OUT = 1, 2   # gnca_rollout_ex_f32 pieces (include/gnca.h)
 PHASE_COMPACT = 16   # rollout mode: K1 packs the live cells' dx per tile, K2 unpacks (include/gnca.h)
 
 _lib = None
@@ -117,6 +119,9 @@ def load(path: str = LIB_PATH):
     lib.gnca_rollout_f32.restype = ctypes.c_int
     lib.gnca_rollout_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights),
                                      ctypes.c_int32, vp, vp, vp, vp, vp, sz, vp]
+    lib.gnca_rollout_ex_f32.restype = ctypes.c_int
+    lib.gnca_rollout_ex_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights),
+                                        ctypes.c_int32, vp, vp, vp, vp, vp, sz, ctypes.c_uint32, vp]
     lib.gnca_rollout_stamped_f32.restype = ctypes.c_int
     lib.gnca_rollout_stamped_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights),
                                              ctypes.c_int32, vp, vp, vp, vp, vp, sz, vp,

@@ -128,14 +128,23 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   return L;
 }
 
+#ifndef GNCA_K1_LEAN
+#define GNCA_K1_LEAN 1   // register-lean group body (one GEMM2 accumulator seeded with the message,
+                         // GEMM1 row blocks double-buffered through GEMM2); 0: round 2's body
+#endif
+
+#ifndef GNCA_K1_SPLIT_NT
+#define GNCA_K1_SPLIT_NT 512   // threads per workgroup of the 16-channel split K1 (768: 3 waves per SIMD)
+#endif
+
 #ifndef GNCA_DMA_WAVES
 #define GNCA_DMA_WAVES 1   // A/B builds: waves (the first failing pulls) sharing the next tile's DMA (3: K1 0.4015-0.4044 vs 0.4008-0.4026 ms with 1)
 #endif
 
 template <int TH, int TW, int RY, int RX, int KU>
-__global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
+__global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_b[];
-  constexpr int C = 16, HD = 128, NT = 512, NW = 8;
+  constexpr int C = 16, HD = 128, NT = GNCA_K1_SPLIT_NT, NW = NT / 64;
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
   constexpr int PSTR = ks_pstr(RHW);
   constexpr int NQ = RHW / 4, NI4 = (NQ + 63) / 64;
@@ -364,6 +373,15 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
     if (tid < 8 * 2 * 16) {
       u32x4 f0, f1, f2;
       split3_x8(w2v, f0, f1, f2);
+#if GNCA_K1_LEAN
+      // the third part is stored halved (exact: a power-of-two scale of a bf16 value): the GEMM2
+      // stack [P2/2; P2/2] adds P2.H0 / 2 to both accumulator halves, which the epilogue sums
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float lo = __uint_as_float(f2[i] << 16) * 0.5f, hi = __uint_as_float(f2[i] & 0xffff0000u) * 0.5f;
+        f2[i] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+      }
+#endif
       *reinterpret_cast<u32x4*>(smem_b + L.w2 + 0 * 4096 + tid * 16) = f0;
       *reinterpret_cast<u32x4*>(smem_b + L.w2 + 1 * 4096 + tid * 16) = f1;
       *reinterpret_cast<u32x4*>(smem_b + L.w2 + 2 * 4096 + tid * 16) = f2;
@@ -543,6 +561,94 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
         for (int kc = 0; kc < 3; ++kc) asm volatile("" ::"v"(yf[kc][0]), "v"(yf[kc][1]), "v"(yf[kc][2]));
       }
 
+#if GNCA_K1_LEAN
+      // -- message: M = WM.G (stacks [M0;M1] G0 + [M2;0] G0 + [M0;M1] G1 + [M0;0] G2), then the
+      //    message term tanh(M + bm S) * gain seeds GEMM2's accumulator (top half; bottom 0) --
+      f32x16 acc2 = {};
+      if constexpr (GRAPH) {
+        f32x16 accm = {};
+        if (!(GNCA_ABLATE & kAblMfma)) {
+          const u32x4 wmA = *reinterpret_cast<const u32x4*>(smem_b + wmA_o);
+          const u32x4 wmB = *reinterpret_cast<const u32x4*>(smem_b + wmB_o);
+          const u32x4 wmC = *reinterpret_cast<const u32x4*>(smem_b + wmC_o);
+          accm = mfma_bx(wmA, g0, accm);
+          accm = mfma_bx(wmB, g0, accm);
+          accm = mfma_bx(wmA, g1, accm);
+          accm = mfma_bx(wmC, g2, accm);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float bm_ = reinterpret_cast<const float*>(smem_b + bml_o)[r];
+          acc2[r] = fast_tanh(fmaf(bm_, S, accm[r] + accm[r + 8])) * ((hz && r < 4) ? 0.f : mgain);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+
+      // -- GEMM1 row block rb (H = W1.Y + b1: bias + 3 k-chunks x 6 products) into acc1[rb & 1],
+      //    then its ReLU / split and its two GEMM2 k-chunks (DL += [P0;P1] H0 + [P2/2;P2/2] H0 +
+      //    [P0;P1] H1 + [P0;P1] H2 into the one accumulator): two row-block accumulators live --
+      f32x16 acc1[2];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        f32x16& ac = acc1[rb & 1];
+        const u32x4 bz = *reinterpret_cast<const u32x4*>(smem_b + L.bias + rb * 512 + r32 * 16);
+        if (GNCA_ABLATE & kAblMfma) {
+          ac = f32x16{};
+        } else {
+          ac = mfma_bx(bz, ones, f32x16{});
+#pragma unroll
+          for (int kc = 0; kc < 3; ++kc) {
+            const int img = L.w1 + (rb * 3 + kc) * 1024 + lane * 16;
+            const u32x4 a0 = *reinterpret_cast<const u32x4*>(smem_b + img);
+            const u32x4 a1 = *reinterpret_cast<const u32x4*>(smem_b + img + 12288);
+            const u32x4 a2 = *reinterpret_cast<const u32x4*>(smem_b + img + 24576);
+            ac = mfma_bx(a0, yf[kc][0], ac);
+            ac = mfma_bx(a0, yf[kc][1], ac);
+            ac = mfma_bx(a1, yf[kc][0], ac);
+            ac = mfma_bx(a0, yf[kc][2], ac);
+            ac = mfma_bx(a2, yf[kc][0], ac);
+            ac = mfma_bx(a1, yf[kc][1], ac);
+          }
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const int s = 2 * rb + ss;
+          float hv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hv[j] = relu_nan(ac[8 * ss + j]);
+          u32x4 h0, h1, h2;
+          split3_x8(hv, h0, h1, h2);
+          if (GNCA_ABLATE & kAblMfma) {
+            asm volatile("" ::"v"(h0), "v"(h1), "v"(h2));
+            continue;
+          }
+          const u32x4 T0 = *reinterpret_cast<const u32x4*>(smem_b + w2T0 + s * 512);
+          const u32x4 T1 = *reinterpret_cast<const u32x4*>(smem_b + w2T1 + s * 512);
+          acc2 = mfma_bx(T0, h0, acc2);
+          acc2 = mfma_bx(T1, h0, acc2);
+          acc2 = mfma_bx(T0, h1, acc2);
+          acc2 = mfma_bx(T0, h2, acc2);
+        }
+      }
+
+      // -- epilogue: dx = dl + tanh(m) * gain (already in acc2's top half) for channels
+      //    c = (r&3) + 8(r>>2) + 4h; the keep mask is the live list itself --
+      if (valid) {
+        // dense: NCHW; compact: [tile][channel][live index]
+        float* ob = compact ? a.out + (size_t)tile * C * NCELL + (size_t)(4 * h) * NCELL + gi
+                            : outb + relcell + (size_t)(4 * h) * HW;
+        const size_t cstr = compact ? (size_t)NCELL : HW;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float v = acc2[r] + acc2[r + 8];
+          if (GNCA_ABLATE & kAblStore) asm volatile("" ::"v"(v));
+          else if (compact && hz3 && r == 3) a.dxa[(size_t)b * HW + cell0 + relcell] = v;   // alpha: dense
+          else ob[(size_t)((r & 3) + 8 * (r >> 2)) * cstr] = v;
+          s1 += v;
+          s2 = fmaf(v, v, s2);
+        }
+      }
+#else
       // -- message: M = WM.G (stacks [M0;M1] G0 + [M2;0] G0 + [M0;M1] G1 + [M0;0] G2) --
       f32x16 accm = {};
       if constexpr (GRAPH) if (!(GNCA_ABLATE & kAblMfma)) {
@@ -625,6 +731,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split(const K1Args a) {
           s2 = fmaf(v, v, s2);
         }
       }
+#endif
       if (!(GNCA_ABLATE & kAblReduce)) {
         double d1 = s1, d2 = s2;
         for (int off = 32; off > 0; off >>= 1) {

@@ -1323,7 +1323,7 @@ struct Variant {
 
 #define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0}
 #define GNCA_SV(th, tw, ry, rx, ku) \
-  {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), 512, 1, \
+  {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
    ks_layout<th, tw, ry, rx>().total}
 #define GNCA_S32V(th, tw, ry, rx, ku) \
   {32, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split32<th, tw, ry, rx, ku>), 512, 2, \
@@ -1423,7 +1423,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
     // too small to give every CU two workgroups' worth of tiles takes the variant with the most
     // tiles instead (measured at B=8, 72^2: 24x36 55 us/step, 8x24 43 us/step)
     const long tiles = (long)d->B * (d->H / v.TH) * (d->W / v.TW);
-    const long fill = 2L * device_cus() * (512 / v.NT);
+    const long fill = 2L * device_cus() * std::max(1, 512 / v.NT);
     if (!fixed_pick) {
       fixed_pick = &v;
       fixed_tiles = tiles;
@@ -1509,7 +1509,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // (large batches only: a small batch's K2 needs thin bands to fill the chip, where unpacking the
   // field costs more than the dx bytes it saves; B=8 72^2: K2 10 -> 18 us)
   P->compact_ok = P->var->split > 0 && P->var->TH > 0 && !msg_only && !attn_on &&
-                  (long)P->total_tiles >= 2L * device_cus() * (512 / P->var->NT);
+                  (long)P->total_tiles >= 2L * device_cus() * std::max(1, 512 / P->var->NT);
   {
     // K2 bands on the compact field: ~12 rows (B=1024 72^2, tables feeding the alpha rows: 4 rows
     // 0.233, 8 0.180, 12 0.170, 24 0.170 ms; since the alpha plane is dense: 6 0.164, 8 0.158,
@@ -1915,8 +1915,10 @@ int gnca_fire_mask_u8(const gnca_step_desc* desc, uint8_t* mask, void* stream) {
 
 static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
                         const int8_t* offsets, const float* x, float* x_final, float* scratch,
-                        void* ws, size_t ws_bytes, void* stream, uint64_t* stamps, int stamp_cap) {
+                        void* ws, size_t ws_bytes, void* stream, uint64_t* stamps, int stamp_cap,
+                        uint32_t flags) {
   if (!desc || steps < 0 || !x || !x_final || !scratch) return GNCA_ERR_INVALID;
+  if (flags & ~(uint32_t)(GNCA_ROLLOUT_ALIVE_IN | GNCA_ROLLOUT_ALIVE_OUT)) return GNCA_ERR_INVALID;
   if (desc->fire_mode != GNCA_FIRE_NONE && desc->fire_mode != GNCA_FIRE_HASH) return GNCA_ERR_INVALID;
   if (x == x_final || x == scratch || x_final == scratch) return GNCA_ERR_INVALID;
   const int k = desc->num_offsets;
@@ -1931,13 +1933,15 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
   // above either threshold keeps its alpha through the post-update gate); and only
   // when every step uses the same threshold pair (one desc for the whole rollout: yes)
   const bool hand_alive = desc->alpha_thr >= 0.f && desc->graph_alpha_thr >= desc->alpha_thr;
+  if ((flags & (GNCA_ROLLOUT_ALIVE_IN | GNCA_ROLLOUT_ALIVE_OUT)) && !hand_alive) return GNCA_ERR_INVALID;
+  const bool in0 = (flags & GNCA_ROLLOUT_ALIVE_IN) != 0, out_last = (flags & GNCA_ROLLOUT_ALIVE_OUT) != 0;
   const float* src = x;
   for (int t = 0; t < steps; ++t) {
     float* dst = ((steps - 1 - t) % 2 == 0) ? x_final : scratch;
     dt.rng_step = desc->rng_step + t;
     if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(dt.offsets, offsets + (size_t)t * 2 * k, 2 * k);
     const int rc = step_impl(&dt, w, src, dst, nullptr, nullptr, ws, ws_bytes, st, GNCA_PHASE_ALL,
-                             nullptr, hand_alive && t > 0, hand_alive && t + 1 < steps, true,
+                             nullptr, hand_alive && (t > 0 || in0), hand_alive && (t + 1 < steps || out_last), true,
                              stamps ? stamps + (size_t)t * 4 * stamp_cap : nullptr, stamp_cap);
     if (rc != GNCA_OK) return rc;
     src = dst;
@@ -1950,7 +1954,13 @@ extern "C" {
 int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
                      const int8_t* offsets, const float* x, float* x_final, float* scratch,
                      void* ws, size_t ws_bytes, void* stream) {
-  return rollout_impl(desc, w, steps, offsets, x, x_final, scratch, ws, ws_bytes, stream, nullptr, 0);
+  return rollout_impl(desc, w, steps, offsets, x, x_final, scratch, ws, ws_bytes, stream, nullptr, 0, 0u);
+}
+
+int gnca_rollout_ex_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
+                        const int8_t* offsets, const float* x, float* x_final, float* scratch,
+                        void* ws, size_t ws_bytes, uint32_t flags, void* stream) {
+  return rollout_impl(desc, w, steps, offsets, x, x_final, scratch, ws, ws_bytes, stream, nullptr, 0, flags);
 }
 
 int gnca_rollout_stamped_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
@@ -1959,7 +1969,7 @@ int gnca_rollout_stamped_f32(const gnca_step_desc* desc, const gnca_weights* w, 
                              void* stream) {
   if (!stamps || stamp_cap <= 0) return GNCA_ERR_INVALID;
   return rollout_impl(desc, w, steps, offsets, x, x_final, scratch, ws, ws_bytes, stream, stamps,
-                      stamp_cap);
+                      stamp_cap, 0u);
 }
 
 }  // extern "C"

@@ -186,6 +186,21 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
                      void* ws, size_t ws_bytes, void* stream);
 
 /*
+ * gnca_rollout_f32 in pieces: a long rollout issued as several calls (the host draws the next
+ * piece's offsets while the device runs the previous piece) computes exactly the one-call result
+ * when the pieces hand the alive masks over through the shared workspace:
+ *   GNCA_ROLLOUT_ALIVE_OUT  the last step's K2 also writes the next state's alive masks into `ws`
+ *   GNCA_ROLLOUT_ALIVE_IN   the first step's K1 reads them from `ws` (written by the previous call
+ *                           with ALIVE_OUT on the same workspace; x = that call's x_final)
+ * Both need 0 <= alpha_thr <= graph_alpha_thr (else GNCA_ERR_INVALID).  flags = 0 is gnca_rollout_f32.
+ */
+#define GNCA_ROLLOUT_ALIVE_IN  (1u << 0)
+#define GNCA_ROLLOUT_ALIVE_OUT (1u << 1)
+int gnca_rollout_ex_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
+                        const int8_t* offsets, const float* x, float* x_final, float* scratch,
+                        void* ws, size_t ws_bytes, uint32_t flags, void* stream);
+
+/*
  * Measurement twin of gnca_rollout_f32: the same launches, and every K1 / K2 workgroup also writes
  * two wall-clock stamps (the 100 MHz s_memrealtime counter: at its first instruction and after its
  * last barrier) into `stamps` (device memory, uint64, zero-initialised by the caller):
