@@ -109,10 +109,10 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
   KSLayout L{};
   int o = 0;
-  L.sp_slot = ks_a16(RHW * 4);
+  L.sp_slot = ks_a16(RHW);
   L.lst_slot = ks_a16(TH * TW * 2);
   L.xs = o; o += 16 * ks_pstr(RHW) * 4;   // first: region reads fit the 16-bit DS offsets
-  L.sp = o; o += 2 * L.sp_slot;           // sender plane (floats), two slots
+  L.sp = o; o += 2 * L.sp_slot;           // sender plane (bytes 0/1), two slots
   L.ab = o; o += ks_a16(RHW);             // the preparer's alive bytes over the region
   L.lst = o; o += 2 * L.lst_slot;         // live-cell list (u16 cell indices), two slots
   L.cnt = o; o += 16;                     // live cells per slot; group counter; staging-reads-done counter
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
     const size_t cell0 = (size_t)i0 * W + j0;
-    float* spp = reinterpret_cast<float*>(smem_b + L.sp + s * L.sp_slot);
+    uint32_t* spp = reinterpret_cast<uint32_t*>(smem_b + L.sp + s * L.sp_slot);
     uint16_t* lstp = reinterpret_cast<uint16_t*>(smem_b + L.lst + s * L.lst_slot);
     uint32_t* abw = reinterpret_cast<uint32_t*>(smem_b + L.ab);
     const uint8_t* abq = reinterpret_cast<const uint8_t*>(smem_b + L.ab);
@@ -259,12 +259,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         const int e = 64 * u + lane;
         if (e < NQA) {
           abw[e] = v[u];
-          if constexpr (GRAPH) {
-            f4 q;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) q[k] = a2a ? (float)((v[u] >> (8 * k + 1)) & 1u) : 1.f;
-            *reinterpret_cast<f4*>(spp + 4 * e) = q;
-          }
+          if constexpr (GRAPH) spp[e] = a2a ? (v[u] >> 1) & 0x01010101u : 0x01010101u;   // 4 sender bytes
         }
       }
     }
@@ -441,7 +436,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const int i0 = ty * TH, j0 = tx * TW;
     const size_t cell0 = (size_t)i0 * W + j0;
     float* outb = a.out + (size_t)b * C * HW + cell0;
-    const float* sp = reinterpret_cast<const float*>(smem_b + L.sp + par * L.sp_slot);
+    const uint8_t* sp = reinterpret_cast<const uint8_t*>(smem_b + L.sp + par * L.sp_slot);
     const uint16_t* lst = reinterpret_cast<const uint16_t*>(smem_b + L.lst + par * L.lst_slot);
     const int nlive = cnt[par];
 
@@ -476,11 +471,11 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
 #pragma unroll
         for (int j = 0; j < 8; ++j) gv[j] = 0.f;
         const float* xq = xs + hb + pidx;
-        const float* spq = sp + pidx;
+        const uint8_t* spq = sp + pidx;
 #pragma unroll
         for (int o = 0; o < KU; ++o) {
           const int d = a.odl[o];
-          const float s_ = spq[-d];
+          const float s_ = (float)spq[-d];
           S += s_;
           const float* xo = xq - d;
 #pragma unroll

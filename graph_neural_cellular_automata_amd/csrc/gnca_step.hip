@@ -1783,6 +1783,83 @@ int gnca_step_masked_phases(const gnca_step_desc* d, const gnca_weights* w, cons
 
 }  // namespace gnca
 
+namespace gnca {
+
+// ---------------------------------------------------------------------------------------------
+// Rollout sub-batch pipeline.  K1 (MFMA/VALU-bound, one persistent workgroup per CU) and K2
+// (HBM-bound) of one step cannot overlap: K2 needs the step's GroupNorm statistics, i.e. every
+// K1 tile of its sample.  Samples are independent, so a large-batch rollout runs as NSUB
+// sub-batches, each stepped on its own stream (the caller's and helper streams) with its own
+// workspace region: sub-batch 1's K1 follows sub-batch 0's K1 onto the CUs, and sub-batch 0's K2
+// runs on the same CUs beside it (the split K1 leaves LDS, registers and wave slots for one K2
+// workgroup per CU), so K2's HBM streaming hides under K1's MFMA work.  Results are bitwise those
+// of the one-stream rollout (per-sample GroupNorm, fire hashed by global sample index).
+// ---------------------------------------------------------------------------------------------
+constexpr int kRolloutSubs = 2;
+
+static void sub_desc(const gnca_step_desc* d, int sub, int nsub, gnca_step_desc* o, int* b0) {
+  *o = *d;
+  const int per = d->B / nsub, rem = d->B % nsub;
+  *b0 = sub * per + std::min(sub, rem);
+  o->B = per + (sub < rem ? 1 : 0);
+  o->sample_base = d->sample_base + *b0;
+}
+
+// sub-batches of a rollout of `d`'s shape: kRolloutSubs when the planned K1 is the 16-channel
+// split kernel with the compact field in every sub-batch and K1 + K2 fit one CU together
+static int rollout_subs(const gnca_step_desc* d) {
+  if (!d || d->B < kRolloutSubs) return 1;
+  Plan P;
+  if (!make_plan(d, false, &P) || P.var->split != 1 || !P.compact_ok) return 1;
+  for (int s = 0; s < kRolloutSubs; ++s) {
+    gnca_step_desc sd;
+    int b0;
+    sub_desc(d, s, kRolloutSubs, &sd, &b0);
+    Plan Q;
+    if (!make_plan(&sd, false, &Q) || Q.var != P.var || !Q.compact_ok) return 1;
+    if (Q.lds1 + Q.lds2_c + 512 > (size_t)max_lds_bytes()) return 1;   // K2's static LDS + margin
+  }
+  return kRolloutSubs;
+}
+
+static size_t sub_ws_bytes(const gnca_step_desc* d, int sub, int nsub) {
+  gnca_step_desc sd;
+  int b0;
+  sub_desc(d, sub, nsub, &sd, &b0);
+  Plan Q;
+  return make_plan(&sd, false, &Q) ? (Q.ws_bytes + 255) & ~(size_t)255 : 0;
+}
+
+// per-device helper streams and fork/join events (created once, never destroyed: the library
+// lives as long as the process)
+struct SubStreams {
+  hipStream_t s[kRolloutSubs];
+  hipEvent_t fork, join[kRolloutSubs];
+  std::mutex mu;   // one rollout's fork .. join enqueue at a time per device
+};
+
+static SubStreams* sub_streams() {
+  static std::mutex mu;
+  static std::unordered_map<int, SubStreams*> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  SubStreams* ss = new SubStreams();
+  ss->s[0] = nullptr;   // sub-batch 0 runs on the caller's stream
+  bool ok = hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) == hipSuccess;
+  for (int k = 0; k < kRolloutSubs && ok; ++k) {
+    if (k > 0) ok = hipStreamCreateWithFlags(&ss->s[k], hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&ss->join[k], hipEventDisableTiming) == hipSuccess;
+  }
+  if (!ok) return nullptr;
+  cache[dev] = ss;
+  return ss;
+}
+
+}  // namespace gnca
+
 using namespace gnca;
 
 extern "C" {
@@ -1808,6 +1885,12 @@ size_t gnca_workspace_bytes(const gnca_step_desc* desc) {
   Plan Q;
   size_t m = P.ws_bytes;
   if ((desc->flags & GNCA_GRAPH) && make_plan(desc, true, &Q) && Q.ws_bytes > m) m = Q.ws_bytes;
+  const int nsub = rollout_subs(desc);
+  if (nsub > 1) {   // a rollout of this shape carves one workspace per sub-batch
+    size_t sum = 0;
+    for (int k = 0; k < nsub; ++k) sum += sub_ws_bytes(desc, k, nsub);
+    if (sum > m) m = sum;
+  }
   return m;
 }
 
@@ -1821,7 +1904,7 @@ int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* 
   else
     snprintf(name, (size_t)n, "gnca_k1_update<%d,%d,%d,%d,%d,%d,%d,%d>", v->CP, v->HDP, v->TH, v->TW, v->RY, v->RX,
              v->KU, v->NT);
-  if (arith) *arith = (v->split ? 1 : 0) | (P.compact_ok ? 2 : 0);
+  if (arith) *arith = (v->split ? 1 : 0) | (P.compact_ok ? 2 : 0) | (rollout_subs(desc) > 1 ? 4 : 0);
   return GNCA_OK;
 }
 
@@ -1935,18 +2018,64 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
   const bool hand_alive = desc->alpha_thr >= 0.f && desc->graph_alpha_thr >= desc->alpha_thr;
   if ((flags & (GNCA_ROLLOUT_ALIVE_IN | GNCA_ROLLOUT_ALIVE_OUT)) && !hand_alive) return GNCA_ERR_INVALID;
   const bool in0 = (flags & GNCA_ROLLOUT_ALIVE_IN) != 0, out_last = (flags & GNCA_ROLLOUT_ALIVE_OUT) != 0;
-  const float* src = x;
-  for (int t = 0; t < steps; ++t) {
-    float* dst = ((steps - 1 - t) % 2 == 0) ? x_final : scratch;
-    dt.rng_step = desc->rng_step + t;
-    if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(dt.offsets, offsets + (size_t)t * 2 * k, 2 * k);
-    const int rc = step_impl(&dt, w, src, dst, nullptr, nullptr, ws, ws_bytes, st, GNCA_PHASE_ALL,
-                             nullptr, hand_alive && (t > 0 || in0), hand_alive && (t + 1 < steps || out_last), true,
-                             stamps ? stamps + (size_t)t * 4 * stamp_cap : nullptr, stamp_cap);
-    if (rc != GNCA_OK) return rc;
-    src = dst;
+  const int nsub = rollout_subs(&dt);
+  if (nsub == 1) {
+    const float* src = x;
+    for (int t = 0; t < steps; ++t) {
+      float* dst = ((steps - 1 - t) % 2 == 0) ? x_final : scratch;
+      dt.rng_step = desc->rng_step + t;
+      if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(dt.offsets, offsets + (size_t)t * 2 * k, 2 * k);
+      const int rc = step_impl(&dt, w, src, dst, nullptr, nullptr, ws, ws_bytes, st, GNCA_PHASE_ALL,
+                               nullptr, hand_alive && (t > 0 || in0), hand_alive && (t + 1 < steps || out_last),
+                               true, stamps ? stamps + (size_t)t * 4 * stamp_cap : nullptr, stamp_cap);
+      if (rc != GNCA_OK) return rc;
+      src = dst;
+    }
+    return GNCA_OK;
   }
-  return GNCA_OK;
+  // sub-batch pipeline (above): sub-batch j on stream j with workspace region j; its launches are
+  // enqueued step-major so every stream always has its next step queued
+  gnca_step_desc sd[kRolloutSubs];
+  size_t off[kRolloutSubs], wsz[kRolloutSubs], elem0[kRolloutSubs];
+  size_t wtot = 0;
+  const size_t per_sample = (size_t)desc->C * desc->H * desc->W;
+  for (int j = 0; j < nsub; ++j) {
+    int b0;
+    sub_desc(&dt, j, nsub, &sd[j], &b0);
+    elem0[j] = (size_t)b0 * per_sample;
+    wsz[j] = sub_ws_bytes(&dt, j, nsub);
+    off[j] = wtot;
+    wtot += wsz[j];
+  }
+  if (!ws || ws_bytes < wtot) return GNCA_ERR_WORKSPACE;
+  SubStreams* ss = sub_streams();
+  if (!ss) return GNCA_ERR_HIP;
+  std::lock_guard<std::mutex> lk(ss->mu);
+  hipStream_t sj[kRolloutSubs];
+  for (int j = 0; j < nsub; ++j) sj[j] = j == 0 ? st : ss->s[j];
+  if (hipEventRecord(ss->fork, st) != hipSuccess) return GNCA_ERR_HIP;
+  for (int j = 1; j < nsub; ++j)
+    if (hipStreamWaitEvent(sj[j], ss->fork, 0) != hipSuccess) return GNCA_ERR_HIP;
+  char* wsb = reinterpret_cast<char*>(ws);
+  int rc = GNCA_OK;
+  for (int t = 0; t < steps && rc == GNCA_OK; ++t) {
+    const float* src = t == 0 ? x : (((steps - t) % 2 == 0) ? x_final : scratch);
+    float* dst = ((steps - 1 - t) % 2 == 0) ? x_final : scratch;
+    for (int j = 0; j < nsub && rc == GNCA_OK; ++j) {
+      sd[j].rng_step = desc->rng_step + t;
+      if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(sd[j].offsets, offsets + (size_t)t * 2 * k, 2 * k);
+      rc = step_impl(&sd[j], w, src + elem0[j], dst + elem0[j], nullptr, nullptr, wsb + off[j], wsz[j], sj[j],
+                     GNCA_PHASE_ALL, nullptr, hand_alive && (t > 0 || in0),
+                     hand_alive && (t + 1 < steps || out_last), true,
+                     stamps ? stamps + ((size_t)t * nsub + j) * 4 * stamp_cap : nullptr, stamp_cap);
+    }
+  }
+  // join (also after a failed launch: the helper streams' work stays ordered before the caller's)
+  for (int j = 1; j < nsub; ++j) {
+    if (hipEventRecord(ss->join[j], sj[j]) != hipSuccess || hipStreamWaitEvent(st, ss->join[j], 0) != hipSuccess)
+      return GNCA_ERR_HIP;
+  }
+  return rc;
 }
 
 extern "C" {

@@ -145,6 +145,15 @@ def rollout_compact(desc: L.StepDesc) -> bool:
     return bool(arith.value & 2)
 
 
+def rollout_subs(desc: L.StepDesc) -> int:
+    """Concurrent sub-batches a rollout of ``desc``'s shape runs as (2: one sub-batch's K2 beside
+    the other's K1 on two streams; 1: one stream)."""
+    buf = ctypes.create_string_buffer(128)
+    arith = ctypes.c_int32(0)
+    L.check(L.load().gnca_k1_variant(ctypes.byref(desc), buf, 128, ctypes.byref(arith)), "gnca_k1_variant")
+    return 2 if arith.value & 4 else 1
+
+
 def stream_ptr(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 

@@ -14,7 +14,8 @@
  *   - All work is stream-ordered on `stream`; no entry point synchronises the device, allocates
  *     memory or copies host<->device, so calls can be captured into a hipGraph.
  *   - Return value: 0 (GNCA_OK) or a negative gnca_status; gnca_status_string() names it.
- *   - Stateless and reentrant.
+ *   - Stateless and reentrant (gnca_rollout_f32's sub-batch streams are per-device helpers whose
+ *     enqueue is serialised by an internal lock).
  *
  * Reference interfaces replaced (paths relative to the reference root):
  *   gnca_step_f32        NeuralCAGraph.forward        src/modules/ncagraph.py:106-168
@@ -119,7 +120,9 @@ size_t gnca_workspace_bytes(const gnca_step_desc* desc);
  * truncated to n bytes), and its MFMA arithmetic in *arith (may be NULL): 0 = fp32 MFMA
  * (v_mfma_f32_*_f32), 1 = bf16 MFMA on exact 3-way splits of the fp32 operands (6 products per
  * fp32 product, gnca_k1_split.h), plus 2 when a rollout of this shape uses the compact update field
- * (GNCA_PHASE_COMPACT).  Host-only.  Returns GNCA_OK or GNCA_ERR_INVALID. */
+ * (GNCA_PHASE_COMPACT), plus 4 when a rollout of this shape runs as 2 concurrent sub-batches (one
+ * stream each: one sub-batch's K2 beside the other's K1; see gnca_rollout_f32).  Host-only.
+ * Returns GNCA_OK or GNCA_ERR_INVALID. */
 int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* arith);
 
 /*
@@ -179,7 +182,12 @@ int gnca_perceive_f32(int32_t B, int32_t C, int32_t H, int32_t W, const float* w
  * A whole no-grad rollout of `steps` CA steps with GNCA_FIRE_HASH (or GNCA_FIRE_NONE) masks:
  * step t uses offsets[t*2*k .. ] (host array, k = desc->num_offsets pairs per step) and
  * rng_step = desc->rng_step + t.  x is read, x_final receives the last state; scratch holds
- * one more state ([B,C,H,W] fp32).  Equivalent to `steps` gnca_step_f32 calls.
+ * one more state ([B,C,H,W] fp32).  Equivalent to `steps` gnca_step_f32 calls.  Large batches
+ * (gnca_k1_variant's arith bit 4) run as 2 sub-batches of samples, each on its own stream forked
+ * from and joined back into `stream` (stream-ordered for the caller, capturable), so that one
+ * sub-batch's memory-bound finalize kernel runs on the CUs beside the other's MFMA kernel; the
+ * results are bitwise those of one stream.  `ws` then holds one workspace per sub-batch
+ * (gnca_workspace_bytes accounts for it).
  */
 int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
                      const int8_t* offsets, const float* x, float* x_final, float* scratch,
@@ -204,7 +212,9 @@ int gnca_rollout_ex_f32(const gnca_step_desc* desc, const gnca_weights* w, int32
  * Measurement twin of gnca_rollout_f32: the same launches, and every K1 / K2 workgroup also writes
  * two wall-clock stamps (the 100 MHz s_memrealtime counter: at its first instruction and after its
  * last barrier) into `stamps` (device memory, uint64, zero-initialised by the caller):
- *   stamps[((t * 2 + k) * stamp_cap + wg) * 2 + {0: start, 1: end}],  t = step, k = 0 (K1) / 1 (K2)
+ *   stamps[(((t * nsub + j) * 2 + k) * stamp_cap + wg) * 2 + {0: start, 1: end}],
+ *   t = step, j = sub-batch (nsub = 2 when gnca_k1_variant's arith has bit 4, else 1),
+ *   k = 0 (K1) / 1 (K2)
  * so a launch's duration is max(end) - min(start) over its workgroups, with no event or marker in
  * the stream between launches.  GNCA_ERR_INVALID if a launch has more than stamp_cap workgroups.
  */

@@ -425,3 +425,46 @@ def test_masked_step_many_tiles_per_workgroup(dev):
     masked, _ = S.step(d, w, x, active=act)
     assert torch.equal(masked[act], full[act])
     assert torch.equal(masked[~act], x[~act])
+
+
+def test_subbatch_rollout_and_pieces_bitwise(dev):
+    """A large-batch rollout runs as 2 sub-batches on two streams (one sub-batch's K2 beside the
+    other's K1): bitwise the states of repeated single steps; and a rollout issued in pieces with the
+    alive masks handed over through the workspace (gnca_rollout_ex_f32 ALIVE_OUT / ALIVE_IN) is
+    bitwise the one-call rollout."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    m = _trained_like(dev, seed=9)
+    B, steps = 192, 5
+    x = _state(B, 16, 72, 72, dev, seed=29)
+    random.seed(19)
+    offs = [random.sample(m.graph.offsets, 8) for _ in range(steps)]
+    w, keep = S.make_weights(dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
+                                  b1=m.update_net[0].bias, w2=m.update_net[2].weight,
+                                  gn_weight=m.norm.weight, gn_bias=m.norm.bias,
+                                  **m.graph.weight_tensors()))
+
+    def desc(t):
+        return S.make_desc(B=B, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[t],
+                           flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                           update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                           fire_mode=L.FIRE_HASH, rng_seed=3, rng_step=t, sample_base=7)
+
+    assert S.rollout_subs(desc(0)) == 2
+    r = S.rollout(desc(0), w, x.contiguous(), steps, offs)
+    cur = x
+    for t in range(steps):
+        cur, _ = S.step(desc(t), w, cur)
+    assert torch.equal(r, cur)
+    # pieces of 2 + 3 steps with the alive hand-over
+    lib = L.load()
+    ws = S.workspace(desc(0), dev)
+    a, b2, scratch = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
+    st = torch.cuda.current_stream().cuda_stream
+    for (s0, n, src, dst, fl) in ((0, 2, x, a, L.ROLLOUT_ALIVE_OUT), (2, 3, a, b2, L.ROLLOUT_ALIVE_IN)):
+        flat = [v for o in offs[s0:s0 + n] for p in o for v in p]
+        arr = (ctypes.c_int8 * len(flat))(*flat)
+        L.check(lib.gnca_rollout_ex_f32(ctypes.byref(desc(s0)), ctypes.byref(w), n, arr, src.data_ptr(),
+                                        dst.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(), fl, st),
+                "gnca_rollout_ex_f32")
+    assert torch.equal(b2, r)

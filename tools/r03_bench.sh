@@ -11,7 +11,7 @@ for c in ${CONFIGS:-c2 c3 c5}; do
   timeout -k 10 300 python bench.py --config $c --no-cpu > gpurun_out/${TAG}_$c.json 2> gpurun_out/${TAG}_$c.err || { echo "bench $c failed"; tail -5 gpurun_out/${TAG}_$c.err; exit 1; }
 done
 for f in gpurun_out/${TAG}_bench.json gpurun_out/${TAG}_c*.json; do
-  python -c "import json; d=json.load(open('$f')); r=d['roofline']; t=d['device_timeline']; print('$f', '%.3e'%d['value'], 'ms/step %.4f'%d['ms_per_step'], 'stamped %.4f span %.4f k1 %.4f k2 %.4f gaps %.4f'%(t['stamped_rollout_ms_per_step'], t['first_k1_start_to_last_k2_end_ms_per_step'], t['k1_ms'], t['k2_ms'], t['gaps_ms_per_step']), 'frac %.3f'%r['frac'])"
+  python -c "import json; d=json.load(open('$f')); r=d['roofline']; t=d['device_timeline']; print('$f', '%.3e'%d['value'], 'ms/step %.4f'%d['ms_per_step'], 'stamped %.4f span %.4f subs %d k1 %.4f k2 %.4f'%(t['stamped_rollout_ms_per_step'], t['first_k1_start_to_last_k2_end_ms_per_step'], t.get('sub_batches',1), t['k1_ms'], t['k2_ms']), 'frac %.3f'%r['frac'])"
 done
 if [ -n "${PROF:-1}" ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof.err || { echo "prof failed"; tail -5 gpurun_out/${TAG}_prof.err; exit 1; }
