@@ -1795,7 +1795,10 @@ namespace gnca {
 // workgroup per CU), so K2's HBM streaming hides under K1's MFMA work.  Results are bitwise those
 // of the one-stream rollout (per-sample GroupNorm, fire hashed by global sample index).
 // ---------------------------------------------------------------------------------------------
-constexpr int kRolloutSubs = 2;
+#ifndef GNCA_ROLLOUT_SUBS
+#define GNCA_ROLLOUT_SUBS 2   // measurement builds: 1 = one stream (no sub-batch pipeline)
+#endif
+constexpr int kRolloutSubs = GNCA_ROLLOUT_SUBS;
 
 static void sub_desc(const gnca_step_desc* d, int sub, int nsub, gnca_step_desc* o, int* b0) {
   *o = *d;
@@ -1808,7 +1811,7 @@ static void sub_desc(const gnca_step_desc* d, int sub, int nsub, gnca_step_desc*
 // sub-batches of a rollout of `d`'s shape: kRolloutSubs when the planned K1 is the 16-channel
 // split kernel with the compact field in every sub-batch and K1 + K2 fit one CU together
 static int rollout_subs(const gnca_step_desc* d) {
-  if (!d || d->B < kRolloutSubs) return 1;
+  if (kRolloutSubs < 2 || !d || d->B < kRolloutSubs) return 1;
   Plan P;
   if (!make_plan(d, false, &P) || P.var->split != 1 || !P.compact_ok) return 1;
   for (int s = 0; s < kRolloutSubs; ++s) {
