@@ -38,10 +38,10 @@ __host__ __device__ constexpr KS32Layout ks32_layout() {
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
   KS32Layout L{};
   int o = 0;
-  L.sp_slot = ks_a16(RHW * 4);
+  L.sp_slot = ks_a16(RHW);
   L.lst_slot = ks_a16(TH * TW * 2);
   L.xs = o; o += 16 * ks_pstr(RHW) * 4;           // one phase's 16 channel planes
-  L.sp = o; o += 2 * L.sp_slot;                   // sender plane, two slots
+  L.sp = o; o += 2 * L.sp_slot;                   // sender plane (bytes 0/1), two slots
   L.ab = o; o += ks_a16(RHW);                     // the preparer's alive bytes over the region
   L.lst = o; o += 2 * L.lst_slot;                 // live-cell list, two slots
   L.cnt = o; o += 16;                             // live cells per slot; staged-reads-done counter
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
     const size_t cell0 = (size_t)i0 * W + j0;
-    float* spp = reinterpret_cast<float*>(smem_b + L.sp + s * L.sp_slot);
+    uint8_t* spp = reinterpret_cast<uint8_t*>(smem_b + L.sp + s * L.sp_slot);
     uint16_t* lstp = reinterpret_cast<uint16_t*>(smem_b + L.lst + s * L.lst_slot);
     uint8_t* abq = reinterpret_cast<uint8_t*>(smem_b + L.ab);
     uint64_t* cb = reinterpret_cast<uint64_t*>(smem_b + L.cb);
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
         const int e = 64 * u + lane;
         if (e < RHW) {
           abq[e] = (uint8_t)v[u];
-          if constexpr (GRAPH) spp[e] = a2a ? (float)((v[u] >> 1) & 1u) : 1.f;
+          if constexpr (GRAPH) spp[e] = a2a ? (uint8_t)((v[u] >> 1) & 1u) : (uint8_t)1;
         }
       }
     }
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     const int i0 = ty * TH, j0 = tx * TW;
     const size_t cell0 = (size_t)i0 * W + j0;
     float* outb = a.out + (size_t)b * C * HW + cell0;
-    const float* sp = reinterpret_cast<const float*>(smem_b + L.sp + par * L.sp_slot);
+    const uint8_t* sp = reinterpret_cast<const uint8_t*>(smem_b + L.sp + par * L.sp_slot);
     const uint16_t* lst = reinterpret_cast<const uint16_t*>(smem_b + L.lst + par * L.lst_slot);
     const int nlive = cnt[par];
     if (wave == PW && nxt < t_end) prep(nxt, par ^ 1);
@@ -333,12 +333,12 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) gv[j] = 0.f;
         const float* xq = xs + hb + pidx;
-        const float* spq = sp + pidx;
+        const uint8_t* spq = sp + pidx;
         float Sp = 0.f;
 #pragma unroll
         for (int o = 0; o < KU; ++o) {
           const int d = a.odl[o];
-          const float s_ = spq[-d];
+          const float s_ = (float)spq[-d];
           Sp += s_;
           const float* xo = xq - d;
 #pragma unroll
@@ -451,6 +451,15 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       // -- per row block rb: GEMM1 (bias + 6 chunks x 6 products), ReLU / split, GEMM2 k-chunks
       //    2rb, 2rb+1 (6 products each; one accumulator for all 32 output channels) --
       f32x16 accD = {};
+#if GNCA_K1_LEAN
+      // the message term tanh(M + bm S) * gain seeds GEMM2's accumulator (accm dies here)
+      if constexpr (GRAPH) {
+        const float* bmp = reinterpret_cast<const float*>(smem_b + L.bml) + 16 * h;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accD[r] = fast_tanh(fmaf(bmp[r], S, accm[r])) * ((hz && r < 4) ? 0.f : mgain);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         const u32x4 bz = *reinterpret_cast<const u32x4*>(smem_b + L.bias + rb * 512 + r32 * 16);
@@ -502,7 +511,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float v = accD[r];
+#if !GNCA_K1_LEAN
           if constexpr (GRAPH) v = fmaf(fast_tanh(fmaf(bmp[r], S, accm[r])), (hz && r < 4) ? 0.f : mgain, v);
+#endif
           if (compact && h == 0 && r == 3) a.dxa[(size_t)b * HW + cell0 + (size_t)(ti * W + tj)] = v;   // alpha: dense
           else ob[(size_t)((r & 3) + 8 * (r >> 2)) * cstr] = v;
           s1 += v;

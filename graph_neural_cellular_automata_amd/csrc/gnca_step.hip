@@ -886,6 +886,12 @@ __device__ __forceinline__ int k2_sample(int j, int B, int zigzag) {
 // the band needs first (GroupNorm partials, alpha rows, gamma/beta and the first KU main items)
 // is issued before the first barrier: a small-batch launch waits out one memory latency, not
 // one per phase.
+// K2's update of one non-alpha value: x + tanh(GN(d)) * gain with GN and the tanh's 2/ln2 folded
+// into (sc, sh) per channel: (x + gain) + (-2 gain) / (2^(d sc + sh) + 1)
+__device__ __forceinline__ float k2_update(float x, float d, float sc, float sh, float gain, float g2) {
+  return fmaf(g2, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(fmaf(d, sc, sh)) + 1.f), x + gain);
+}
+
 template <int V, bool COMPACT>
 __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_norm) {
   typedef float vf __attribute__((ext_vector_type(V)));
@@ -993,6 +999,17 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   __syncthreads();
   const float mu = sh_norm[0], rs = sh_norm[1];
   const float g3 = gn ? gsh[3] : 1.f, b3 = gn ? gsh[32 + 3] : 0.f;
+  // the non-alpha channels' update, folded: x + tanh(z) * gain = (x + gain) - 2 gain / (2^(z log2 e * 2) + 1)
+  // with z = GN(d) = d * gamma rs + (beta - mu gamma rs); per channel k2s[c] = 2 log2(e) gamma rs,
+  // k2s[32 + c] = 2 log2(e) (beta - mu gamma rs) (written here, read after the next barrier)
+  float* k2s = sh_norm + 4 + 64;
+  constexpr float kL2E2 = 2.8853900817779268f;   // 2 / ln 2
+  if (tid < C) {
+    const float gr = gn ? gsh[tid] * rs : 1.f;
+    k2s[tid] = gr * kL2E2;
+    k2s[32 + tid] = (gn ? fmaf(-mu, gr, gsh[32 + tid]) : 0.f) * kL2E2;
+  }
+  const float g2 = -2.f * a.gain;
 
   // (3) updated alpha over band + halo, then the post-update alive mask (3x3 max-pool, -inf pad)
   auto alpha_at = [&](float xa, float d) {
@@ -1044,13 +1061,9 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
 #pragma unroll
         for (int k = 0; k < V; ++k) v[k] = at[(r0 - h0) * W + V * q + k] * post[V * q + k];
       } else {
-        const float gc = gn ? gsh[c] * rs : 1.f, bc = gn ? gsh[32 + c] : 0.f;
+        const float sc = k2s[c], sh = k2s[32 + c];
 #pragma unroll
-        for (int k = 0; k < V; ++k) {
-          float d = dv[u][k];
-          if (gn) d = (d - mu) * gc + bc;
-          v[k] = xv[u][k] + fast_tanh(d) * a.gain;
-        }
+        for (int k = 0; k < V; ++k) v[k] = k2_update(xv[u][k], dv[u][k], sc, sh, a.gain, g2);
       }
       *reinterpret_cast<vf*>(ob + p) = v;
     }
@@ -1083,31 +1096,33 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
         for (int k = 0; k < V; ++k) v[k] = at[(r0 - h0) * W + e + k] * post[e + k];
         *reinterpret_cast<vf*>(ob + 3 * HW + p0) = v;
       }
+      // the packed values of the vector's live cells are contiguous: one (dword-aligned) vector load
+      // per channel, placed by rank with lane masks that are the same in every channel (reading up
+      // to V-1 floats past the live ones stays inside the workspace: the dx field is followed by
+      // the GroupNorm partials)
+      typedef float vfu __attribute__((ext_vector_type(V), aligned(4)));
       constexpr int CU = 5;   // channels in flight per thread (B=1024 72^2: 3 0.164, 5 0.159, 8 0.183 ms)
       for (int c0 = 0; c0 < C; c0 += CU) {
-        vf xq[CU];
-        float f[CU][V];
+        vf xq[CU], fq[CU];
 #pragma unroll
         for (int u = 0; u < CU; ++u) {
           const int c = c0 + u;
           if (c >= C || c == 3) continue;
           xq[u] = *reinterpret_cast<const vf*>(xb + (size_t)c * HW + p0);
-#pragma unroll
-          for (int k = 0; k < V; ++k) f[u][k] = k < cnt ? src[(size_t)c * NCELL + k] : 0.f;
+          fq[u] = *reinterpret_cast<const vfu*>(src + (size_t)c * NCELL);
         }
 #pragma unroll
         for (int u = 0; u < CU; ++u) {
           const int c = c0 + u;
           if (c >= C || c == 3) continue;
-          const float gc = gn ? gsh[c] * rs : 1.f, bc = gn ? gsh[32 + c] : 0.f;
+          const float sc = k2s[c], sh = k2s[32 + c];
           vf v;
 #pragma unroll
           for (int k = 0; k < V; ++k) {
             float d = 0.f;
 #pragma unroll
-            for (int r = 0; r <= k; ++r) d = rk[k] == r ? f[u][r] : d;
-            if (gn) d = (d - mu) * gc + bc;
-            v[k] = xq[u][k] + fast_tanh(d) * a.gain;
+            for (int r = 0; r <= k; ++r) d = rk[k] == r ? fq[u][r] : d;
+            v[k] = k2_update(xq[u][k], d, sc, sh, a.gain, g2);
           }
           *reinterpret_cast<vf*>(ob + (size_t)c * HW + p0) = v;
         }
@@ -1128,7 +1143,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
 template <int V, bool COMPACT>
 __global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ float sh_norm[4 + 64];
+  __shared__ float sh_norm[4 + 64 + 64];
   const int tid = threadIdx.x;
   wg_stamp(a.stamps, 0);
   const int bj = blockIdx.x / a.nbands, band = blockIdx.x - bj * a.nbands;
