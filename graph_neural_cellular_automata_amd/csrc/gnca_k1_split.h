@@ -137,6 +137,10 @@ __host__ __device__ constexpr KSLayout ks_layout() {
 #define GNCA_K1_SPLIT_NT 512   // threads per workgroup of the 16-channel split K1 (768: 3 waves per SIMD)
 #endif
 
+#ifndef GNCA_K1_PRIO
+#define GNCA_K1_PRIO 0   // wave issue priority of K1 (s_setprio): > 0 favours K1 over a co-resident K2
+#endif
+
 #ifndef GNCA_DMA_WAVES
 #define GNCA_DMA_WAVES 1   // A/B builds: waves (the first failing pulls) sharing the next tile's DMA (3: K1 0.4015-0.4044 vs 0.4008-0.4026 ms with 1)
 #endif
@@ -173,6 +177,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   wg_stamp(a.stamps, 0);
+  if (GNCA_K1_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO);
   const int h = lane >> 5, r32 = lane & 31, c16 = lane & 15;
   const int H = a.H, W = a.W;
   const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
