@@ -515,6 +515,13 @@ def main():
             L.check(rc, "gnca_rollout_ex_f32")
             cur = nxt
 
+    # buffers of the stamped re-run (below), allocated before the GPU warm-up: an allocation between
+    # the warm-up and the timed run (or between the timed and the stamped run) idles the GPU, and the
+    # run after it starts at ramping clocks
+    cap = 16384
+    nsub = S.rollout_subs(make_desc(wl, B, H, H, offsets_table[:K], rank, args.warmup))
+    stamps = torch.zeros(args.steps * nsub * 4 * cap, dtype=torch.int64, device=dev)
+    dst2 = torch.empty_like(x)
     # warmup: the rollout's first W steps, untimed; the K timed steps continue from their state (and
     # fire counters), as one rollout of W + K steps
     start = x
@@ -551,13 +558,6 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t_s) * 1e3 / args.steps
 
-    # buffers of the stamped re-run (below), allocated before the timed region: an allocation between
-    # the two runs would idle the GPU and the re-run would start at ramping clocks
-    cap = 16384
-    nsub = S.rollout_subs(make_desc(wl, B, H, H, offsets_table[:K], rank, args.warmup))
-    stamps = torch.zeros(args.steps * nsub * 4 * cap, dtype=torch.int64, device=dev)
-    dst2 = torch.empty_like(x)
-    torch.cuda.synchronize()
     timed_offsets = []
     t0 = time.perf_counter()
     rollout(args.steps, args.warmup, start, out, record=timed_offsets)

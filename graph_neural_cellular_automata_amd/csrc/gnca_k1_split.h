@@ -128,17 +128,112 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   return L;
 }
 
+// The 16-channel split K1's weight images (bf16 parts in MFMA fragment order, layout ks_layout's
+// w1 .. bml block, offsets relative to its start): W1 [part][rb][kc][lane] x 16 B, the bias, W2
+// [part][s][h][channel] (the third part halved in the lean body), WM [part][h][channel] + a zero
+// image, the message bias per (h, r).  Built by each K1 workgroup into LDS, or once per rollout
+// into global memory (gnca_ks_images) that K1 then copies with LDS-DMA: the same bits either way.
+// NT threads, every weight load of a thread in flight before its splits and stores.
+template <int NT, bool GRAPH, bool TO_LDS>
+__device__ __forceinline__ void ks_fill_images(const K1Args& a, char* dst, int tid);
+
 #ifndef GNCA_K1_LEAN
 #define GNCA_K1_LEAN 1   // register-lean group body (one GEMM2 accumulator seeded with the message,
                          // GEMM1 row blocks double-buffered through GEMM2); 0: round 2's body
 #endif
+
+template <int NT, bool GRAPH, bool TO_LDS>
+__device__ __forceinline__ void ks_fill_images(const K1Args& a, char* dst, int tid) {
+  constexpr int C = 16, HD = 128;
+  constexpr KSLayout L = ks_layout<24, 36, 4, 4>();   // the image block's offsets do not depend on the tile
+  constexpr int OW1 = 0, OB = L.bias - L.w1, OW2 = L.w2 - L.w1, OWM = L.wm - L.w1, OWZ = L.wz - L.w1,
+                OBM = L.bml - L.w1;
+  static_assert(4 * 3 * 64 <= 2 * NT && 8 * 2 * 16 <= NT, "one pass of weight loads");
+  auto st16 = [&](int off, u32x4 v) { *reinterpret_cast<u32x4*>(dst + off) = v; };
+  float w1v[2][8], w2v[8], wmv[8], b1v = 0.f, bmv = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    // W1: entry e = (rb, kc, lane): W1[32rb + (lane&31)][16kc + 8(lane>>5) + 0..7]
+    const int e = tid + u * NT, rb = e / 192, kc = (e / 64) % 3, l = e & 63;
+    const float* src = a.w1 + (size_t)(32 * rb + (l & 31)) * 48 + 16 * kc + 8 * (l >> 5);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w1v[u][j] = e < 4 * 3 * 64 ? src[j] : 0.f;
+  }
+  {
+    // W2: entry (s, h, c): W2[c][32(s>>1) + 16(s&1) + 8(j>>2) + 4h + (j&3)], j = 0..7
+    const int s = (tid >> 5) & 7, hh = (tid >> 4) & 1, c = tid & 15;
+    const float* src = a.w2 + (size_t)c * HD + 32 * (s >> 1) + 16 * (s & 1) + 4 * hh;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w2v[j] = tid < 8 * 2 * 16 ? src[8 * (j >> 2) + (j & 3)] : 0.f;
+    // WM: entry (h, c): WM[c][8h + 0..7]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wmv[j] = (GRAPH && tid < 32) ? a.wm[(tid & 15) * C + 8 * ((tid >> 4) & 1) + j] : 0.f;
+  }
+  if (tid < 128) b1v = a.b1[tid];
+  if (GRAPH && tid < 16) bmv = a.bm[(tid & 3) + 8 * ((tid & 7) >> 2) + 4 * (tid >> 3)];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = tid + u * NT;
+    if (e < 4 * 3 * 64) {
+      const int rb = e / 192, kc = (e / 64) % 3, l = e & 63;
+      u32x4 f0, f1, f2;
+      split3_x8(w1v[u], f0, f1, f2);
+      const int img = OW1 + (rb * 3 + kc) * 1024 + l * 16;
+      st16(img, f0);
+      st16(img + 12288, f1);
+      st16(img + 2 * 12288, f2);
+    }
+  }
+  if (tid < 128) {   // bias: entry (rb, row): k slots 0..2 = the parts of b1[32rb + row]
+    uint32_t p0, p1, p2;
+    split3_pair(b1v, 0.f, p0, p1, p2);
+    u32x4 f;
+    f[0] = (p0 & 0xffffu) | (p1 << 16);
+    f[1] = p2 & 0xffffu;
+    f[2] = 0u;
+    f[3] = 0u;
+    st16(OB + tid * 16, f);
+  }
+  if (tid < 8 * 2 * 16) {
+    u32x4 f0, f1, f2;
+    split3_x8(w2v, f0, f1, f2);
+#if GNCA_K1_LEAN
+    // the third part is stored halved (exact: a power-of-two scale of a bf16 value): the GEMM2
+    // stack [P2/2; P2/2] adds P2.H0 / 2 to both accumulator halves, which the epilogue sums
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float lo = __uint_as_float(f2[i] << 16) * 0.5f, hi = __uint_as_float(f2[i] & 0xffff0000u) * 0.5f;
+      f2[i] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+    }
+#endif
+    st16(OW2 + tid * 16, f0);
+    st16(OW2 + 4096 + tid * 16, f1);
+    st16(OW2 + 8192 + tid * 16, f2);
+  }
+  if (tid < 32) {   // WM, then the zero image
+    u32x4 f0, f1, f2;
+    split3_x8(wmv, f0, f1, f2);
+    st16(OWM + tid * 16, f0);
+    st16(OWM + 512 + tid * 16, f1);
+    st16(OWM + 1024 + tid * 16, f2);
+    st16(OWZ + tid * 16, u32x4{0u, 0u, 0u, 0u});
+  }
+  // message bias of output channel c = (r&3) + 8(r>>2) + 4h at [h][r]
+  if (tid < 16) reinterpret_cast<float*>(dst + OBM)[tid] = bmv;
+}
+
+// The weight images of a rollout, once, into global memory (K1Args::wimg); one 512-thread block.
+__global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst) {
+  if ((a.flags & kGraphOn) != 0) ks_fill_images<512, true, false>(a, dst, threadIdx.x);
+  else ks_fill_images<512, false, false>(a, dst, threadIdx.x);
+}
 
 #ifndef GNCA_K1_SPLIT_NT
 #define GNCA_K1_SPLIT_NT 512   // threads per workgroup of the 16-channel split K1 (768: 3 waves per SIMD)
 #endif
 
 #ifndef GNCA_K1_PRIO
-#define GNCA_K1_PRIO 0   // wave issue priority of K1 (s_setprio): > 0 favours K1 over a co-resident K2
+#define GNCA_K1_PRIO 2   // wave issue priority of K1 (s_setprio): > 0 favours K1 over a co-resident K2
 #endif
 
 #ifndef GNCA_DMA_WAVES
@@ -322,80 +417,24 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   // splits and LDS stores (B=8 72^2 K1: 20.0 -> 19.8 us; the preparer after the weight loads 22.3 us)
   if (tile < t_end) issue_dma(tile, wave, NW);
   if (wave == PW && tile < t_end) prep(tile, 0);
-  static_assert(4 * 3 * 64 <= 2 * NT && 8 * 2 * 16 <= NT && C * 27 <= NT, "one pass of weight loads");
-  float w1v[2][8], w2v[8], wmv[8], b1v = 0.f, bmv = 0.f, pcv = 0.f;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    // W1: entry e = (rb, kc, lane): W1[32rb + (lane&31)][16kc + 8(lane>>5) + 0..7]
-    const int e = tid + u * NT, rb = e / 192, kc = (e / 64) % 3, l = e & 63;
-    const float* src = a.w1 + (size_t)(32 * rb + (l & 31)) * 48 + 16 * kc + 8 * (l >> 5);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) w1v[u][j] = e < 4 * 3 * 64 ? src[j] : 0.f;
-  }
-  {
-    // W2: entry (s, h, c): W2[c][32(s>>1) + 16(s&1) + 8(j>>2) + 4h + (j&3)], j = 0..7
-    const int s = (tid >> 5) & 7, hh = (tid >> 4) & 1, c = tid & 15;
-    const float* src = a.w2 + (size_t)c * HD + 32 * (s >> 1) + 16 * (s & 1) + 4 * hh;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) w2v[j] = tid < 8 * 2 * 16 ? src[8 * (j >> 2) + (j & 3)] : 0.f;
-    // WM: entry (h, c): WM[c][8h + 0..7]
-#pragma unroll
-    for (int j = 0; j < 8; ++j) wmv[j] = (GRAPH && tid < 32) ? a.wm[(tid & 15) * C + 8 * ((tid >> 4) & 1) + j] : 0.f;
-  }
-  if (tid < 128) b1v = a.b1[tid];
-  if (GRAPH && tid < 16) bmv = a.bm[(tid & 3) + 8 * ((tid & 7) >> 2) + 4 * (tid >> 3)];
+  float pcv = 0.f;
   if (tid < C * 27) pcv = a.perc[tid];
   if (tid == 0) { *gctr = 0; *xsd = 0; }
   if (!(GNCA_ABLATE & kAblFill)) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + u * NT;
-      if (e < 4 * 3 * 64) {
-        const int rb = e / 192, kc = (e / 64) % 3, l = e & 63;
-        u32x4 f0, f1, f2;
-        split3_x8(w1v[u], f0, f1, f2);
-        const int img = (rb * 3 + kc) * 1024 + l * 16;
-        *reinterpret_cast<u32x4*>(smem_b + L.w1 + 0 * 12288 + img) = f0;
-        *reinterpret_cast<u32x4*>(smem_b + L.w1 + 1 * 12288 + img) = f1;
-        *reinterpret_cast<u32x4*>(smem_b + L.w1 + 2 * 12288 + img) = f2;
+    if (a.wimg) {
+      // the rollout's weight images, built once (gnca_ks_images): one LDS-DMA copy of the block
+      constexpr int NQI = (L.total - L.w1) / 16;
+      static_assert((L.total - L.w1) % 16 == 0 && L.w1 % 16 == 0, "16-byte image block");
+#pragma unroll 1
+      for (int i = wave; i < (NQI + 63) / 64; i += NW) {
+        const int q = 64 * i + lane;
+        if (q < NQI)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.wimg + 16 * q),
+                                           (__attribute__((address_space(3))) void*)(smem_b + L.w1 + 1024 * i), 16, 0, 0);
       }
+    } else {
+      ks_fill_images<NT, GRAPH, true>(a, smem_b + L.w1, tid);
     }
-    if (tid < 128) {   // bias: entry (rb, row): k slots 0..2 = the parts of b1[32rb + row]
-      uint32_t p0, p1, p2;
-      split3_pair(b1v, 0.f, p0, p1, p2);
-      u32x4 f;
-      f[0] = (p0 & 0xffffu) | (p1 << 16);
-      f[1] = p2 & 0xffffu;
-      f[2] = 0u;
-      f[3] = 0u;
-      *reinterpret_cast<u32x4*>(smem_b + L.bias + tid * 16) = f;
-    }
-    if (tid < 8 * 2 * 16) {
-      u32x4 f0, f1, f2;
-      split3_x8(w2v, f0, f1, f2);
-#if GNCA_K1_LEAN
-      // the third part is stored halved (exact: a power-of-two scale of a bf16 value): the GEMM2
-      // stack [P2/2; P2/2] adds P2.H0 / 2 to both accumulator halves, which the epilogue sums
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float lo = __uint_as_float(f2[i] << 16) * 0.5f, hi = __uint_as_float(f2[i] & 0xffff0000u) * 0.5f;
-        f2[i] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
-      }
-#endif
-      *reinterpret_cast<u32x4*>(smem_b + L.w2 + 0 * 4096 + tid * 16) = f0;
-      *reinterpret_cast<u32x4*>(smem_b + L.w2 + 1 * 4096 + tid * 16) = f1;
-      *reinterpret_cast<u32x4*>(smem_b + L.w2 + 2 * 4096 + tid * 16) = f2;
-    }
-    if (tid < 32) {   // WM, then the zero image
-      u32x4 f0, f1, f2;
-      split3_x8(wmv, f0, f1, f2);
-      *reinterpret_cast<u32x4*>(smem_b + L.wm + 0 * 512 + tid * 16) = f0;
-      *reinterpret_cast<u32x4*>(smem_b + L.wm + 1 * 512 + tid * 16) = f1;
-      *reinterpret_cast<u32x4*>(smem_b + L.wm + 2 * 512 + tid * 16) = f2;
-      *reinterpret_cast<u32x4*>(smem_b + L.wz + tid * 16) = u32x4{0u, 0u, 0u, 0u};
-    }
-    // message bias of output channel c = (r&3) + 8(r>>2) + 4h at [h][r]
-    if (tid < 16) reinterpret_cast<float*>(smem_b + L.bml)[tid] = bmv;
     // the perception zero tap: every channel plane's pad floats (never written by the staging)
     for (int e = tid; e < 16 * (PSTR - RHW); e += NT) xs[(e / (PSTR - RHW)) * PSTR + RHW + e % (PSTR - RHW)] = 0.f;
   }
@@ -464,7 +503,9 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       const bool valid = gi < nlive;
       const int n = lst[valid ? gi : 0];
       const int ti = n / TW, tj = n - (n / TW) * TW;
-      const int pidx = (RY + ti) * RW + (RX + tj);
+      // (GNCA_ABLATE & 8192: timing only, conflict-free stand-in addresses: lane r32 reads region
+      //  cell RY*RW + RX + r32, so the 32 lanes of a half hit 32 distinct banks for every tap)
+      const int pidx = (GNCA_ABLATE & 8192) ? RY * RW + RX + r32 : (RY + ti) * RW + (RX + tj);
       const int hb = 8 * h * PSTR;          // this lane's channel half
       const int relcell = ti * W + tj;
 

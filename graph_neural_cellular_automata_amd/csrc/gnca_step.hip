@@ -167,6 +167,7 @@ struct K1Args {
   float fire_rate, alpha_thr, graph_alpha_thr, message_gain, uniform_w;
   uint32_t flags;
   uint64_t* stamps;    // measurement only (null in product launches): per-workgroup wall-clock stamps
+  const char* wimg;    // split K1: the weight images built once per rollout (gnca_ks_images), or null
   int odl[GNCA_MAX_OFFSETS];   // gather source delta in the staged region: dy*RW + dx (pad: dy*RW)
 };
 
@@ -1388,7 +1389,7 @@ struct Plan {
   int band_c, nbands_c, total2_c;   // K2 on the compact update field
   size_t lds2_c;
   // workspace carve (bytes)
-  size_t off_dx, off_stats, off_mm, off_offw, off_alive, off_rmask, off_rpre, off_dxa, ws_bytes;
+  size_t off_dx, off_stats, off_mm, off_offw, off_alive, off_rmask, off_rpre, off_dxa, off_wimg, ws_bytes;
   bool compact_ok;   // the rollout's compact update field (the bf16-split K1s, large batches)
 };
 
@@ -1544,6 +1545,8 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->off_rmask = carve(P->compact_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint64_t) : 0);
   P->off_rpre = carve(P->compact_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint32_t) : 0);
   P->off_dxa = carve(P->compact_ok ? (size_t)d->B * d->H * d->W * sizeof(float) : 0);
+  // the rollout's weight images of the 16-channel split K1 (built once per rollout, gnca_ks_images)
+  P->off_wimg = carve(P->var->split == 1 ? (size_t)(ks_layout<24, 36, 4, 4>().total - ks_layout<24, 36, 4, 4>().w1) : 0);
   P->ws_bytes = o;
   if (P->need_k0) {
     const size_t k0 = ((size_t)d->C * d->H + d->C + d->d_model + P->k) * sizeof(double);
@@ -1695,7 +1698,7 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
                      const void* fire, float* attn, void* ws, size_t ws_bytes, hipStream_t st,
                      uint32_t phases = GNCA_PHASE_ALL, const uint8_t* active = nullptr,
                      bool alive_in = false, bool alive_out = false, bool compact = false,
-                     uint64_t* stamps = nullptr, int stamp_cap = 0) {
+                     uint64_t* stamps = nullptr, int stamp_cap = 0, const char* wimg = nullptr) {
   Plan P;
   if (!make_plan(d, false, &P)) {
     if (d && d->C >= 4 && d->hidden > 0 && !find_variant(d->C, d->hidden)) return GNCA_ERR_UNSUPPORTED;
@@ -1745,6 +1748,7 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   }
   // measurement: K1's workgroups stamp into stamps[0 .. 2*cap), K2's into stamps[2*cap .. 4*cap)
   k1.stamps = stamps;
+  k1.wimg = P.var->split == 1 ? wimg : nullptr;
   if (stamps && (long)std::min<long>((long)device_cus() * occupancy(P.var->fn, P.lds1, P.var->NT),
                                      P.total_tiles) > stamp_cap)
     return GNCA_ERR_INVALID;
@@ -1810,6 +1814,9 @@ namespace gnca {
 // workgroup per CU), so K2's HBM streaming hides under K1's MFMA work.  Results are bitwise those
 // of the one-stream rollout (per-sample GroupNorm, fire hashed by global sample index).
 // ---------------------------------------------------------------------------------------------
+#ifndef GNCA_ROLLOUT_IMAGES
+#define GNCA_ROLLOUT_IMAGES 1   // measurement builds: 0 = every K1 launch builds its weight images
+#endif
 #ifndef GNCA_ROLLOUT_SUBS
 #define GNCA_ROLLOUT_SUBS 2   // measurement builds: 1 = one stream (no sub-batch pipeline)
 #endif
@@ -2037,6 +2044,25 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
   if ((flags & (GNCA_ROLLOUT_ALIVE_IN | GNCA_ROLLOUT_ALIVE_OUT)) && !hand_alive) return GNCA_ERR_INVALID;
   const bool in0 = (flags & GNCA_ROLLOUT_ALIVE_IN) != 0, out_last = (flags & GNCA_ROLLOUT_ALIVE_OUT) != 0;
   const int nsub = rollout_subs(&dt);
+  // the 16-channel split K1's weight images, once for the whole rollout (every K1 launch then copies
+  // them into LDS with LDS-DMA instead of loading, splitting and storing the fp32 weights)
+  const char* wimg = nullptr;
+  {
+    gnca_step_desc d0 = dt;
+    int b0 = 0;
+    if (nsub > 1) sub_desc(&dt, 0, nsub, &d0, &b0);
+    Plan P0;
+    if (!make_plan(&d0, false, &P0)) return GNCA_ERR_INVALID;
+    if (GNCA_ROLLOUT_IMAGES && P0.var->split == 1 && ws && ws_bytes >= P0.ws_bytes && weights_ok(&d0, w, false, P0)) {
+      K1Args ka;
+      fill_k1(ka, &d0, w, P0, x, nullptr, nullptr, nullptr, reinterpret_cast<char*>(ws));
+      char* dst = reinterpret_cast<char*>(ws) + P0.off_wimg;
+      hipLaunchKernelGGL(gnca_ks_images, dim3(1), dim3(512), 0, st, ka, dst);
+      const int rc = check_launch();
+      if (rc != GNCA_OK) return rc;
+      wimg = dst;
+    }
+  }
   if (nsub == 1) {
     const float* src = x;
     for (int t = 0; t < steps; ++t) {
@@ -2045,7 +2071,7 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
       if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(dt.offsets, offsets + (size_t)t * 2 * k, 2 * k);
       const int rc = step_impl(&dt, w, src, dst, nullptr, nullptr, ws, ws_bytes, st, GNCA_PHASE_ALL,
                                nullptr, hand_alive && (t > 0 || in0), hand_alive && (t + 1 < steps || out_last),
-                               true, stamps ? stamps + (size_t)t * 4 * stamp_cap : nullptr, stamp_cap);
+                               true, stamps ? stamps + (size_t)t * 4 * stamp_cap : nullptr, stamp_cap, wimg);
       if (rc != GNCA_OK) return rc;
       src = dst;
     }
@@ -2085,7 +2111,7 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
       rc = step_impl(&sd[j], w, src + elem0[j], dst + elem0[j], nullptr, nullptr, wsb + off[j], wsz[j], sj[j],
                      GNCA_PHASE_ALL, nullptr, hand_alive && (t > 0 || in0),
                      hand_alive && (t + 1 < steps || out_last), true,
-                     stamps ? stamps + ((size_t)t * nsub + j) * 4 * stamp_cap : nullptr, stamp_cap);
+                     stamps ? stamps + ((size_t)t * nsub + j) * 4 * stamp_cap : nullptr, stamp_cap, wimg);
     }
   }
   // join (also after a failed launch: the helper streams' work stays ordered before the caller's)

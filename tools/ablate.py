@@ -17,7 +17,7 @@ VARIANTS = {
     "no_planes": 32, "mfma_only": 1 | 2 | 4 | 16 | 32, "no_mfma_no_store": 8 | 16,
     "stage_only": 2 | 4 | 8 | 16 | 32,
     "no_fire": 64, "no_zero": 128, "no_reduce": 256,
-    "no_prep": 2048, "no_prep_no_stage": 2049, "no_tiles": 512, "no_tiles_no_fill": 512 | 1024, "lds_lite": 4096,
+    "no_prep": 2048, "no_prep_no_stage": 2049, "no_tiles": 512, "no_tiles_no_fill": 512 | 1024, "lds_lite": 4096, "lds_linear": 8192,
     "bare": 2 | 4 | 8 | 16 | 32 | 64 | 128 | 256, "bare_no_stage": 1 | 2 | 4 | 8 | 16 | 32 | 64 | 128 | 256,
 }
 
