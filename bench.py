@@ -494,10 +494,14 @@ def main():
         """n steps from src into dst, issued in pieces of PIECE steps (gnca_rollout_ex_f32 with the
         alive masks handed over between pieces: bitwise the one-call rollout): the host draws the
         next piece's offsets (graph_augmentation.py:121, timed) while the device runs this one."""
-        npieces = (n + PIECE - 1) // PIECE
+        sizes = []   # 1, 2, 4, ... PIECE steps: only the first (one-step) draw is exposed
+        while sum(sizes) < n:
+            sizes.append(min(1 if not sizes else min(2 * sizes[-1], PIECE), n - sum(sizes)))
+        npieces = len(sizes)
         cur = src
         for p in range(npieces):
-            m = min(PIECE, n - p * PIECE)
+            m = sizes[p]
+            s0 = sum(sizes[:p])
             flat = []
             if graph:
                 for _ in range(m):
@@ -506,7 +510,7 @@ def main():
             if record is not None:
                 record.extend(flat)
             arr = (ctypes.c_int8 * len(flat))(*flat) if flat else None
-            d = make_desc(wl, B, H, H, offsets_table[:K], rank, step0 + p * PIECE)
+            d = make_desc(wl, B, H, H, offsets_table[:K], rank, step0 + s0)
             nxt = dst if (npieces - 1 - p) % 2 == 0 else tmp
             fl = (L.ROLLOUT_ALIVE_IN if p > 0 else 0) | (L.ROLLOUT_ALIVE_OUT if p + 1 < npieces else 0)
             rc = lib.gnca_rollout_ex_f32(ctypes.byref(d), ctypes.byref(w), m, arr, cur.data_ptr(),

@@ -567,8 +567,10 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
             if (GNCA_ABLATE & 4096)
               asm volatile("" : "+v"(n0), "+v"(n1), "+v"(n2), "+v"(n3), "+v"(n4), "+v"(n5), "+v"(n6), "+v"(n7), "+v"(n8));
             y0[j] = n4;
-            y1[j] = (fmaf(2.f, n3, n0) + n6) - (fmaf(2.f, n5, n2) + n8);
-            y2[j] = (fmaf(2.f, n1, n0) + n2) - (fmaf(2.f, n7, n6) + n8);
+            // Sobel-x / -y with shared diagonal differences: 8 VALU instead of 10
+            const float dg = n0 - n8, da = n2 - n6;
+            y1[j] = fmaf(2.f, n3 - n5, dg - da);
+            y2[j] = fmaf(2.f, n1 - n7, dg + da);
           }
         } else {
 #pragma unroll 1

@@ -2054,12 +2054,16 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
     Plan P0;
     if (!make_plan(&d0, false, &P0)) return GNCA_ERR_INVALID;
     if (GNCA_ROLLOUT_IMAGES && P0.var->split == 1 && ws && ws_bytes >= P0.ws_bytes && weights_ok(&d0, w, false, P0)) {
-      K1Args ka;
-      fill_k1(ka, &d0, w, P0, x, nullptr, nullptr, nullptr, reinterpret_cast<char*>(ws));
+      // a continuation piece (ALIVE_IN) reuses the images its first piece built in the same workspace
+      // (rebuilding them here could overwrite them under the other sub-batch stream's K1)
       char* dst = reinterpret_cast<char*>(ws) + P0.off_wimg;
-      hipLaunchKernelGGL(gnca_ks_images, dim3(1), dim3(512), 0, st, ka, dst);
-      const int rc = check_launch();
-      if (rc != GNCA_OK) return rc;
+      if (!in0) {
+        K1Args ka;
+        fill_k1(ka, &d0, w, P0, x, nullptr, nullptr, nullptr, reinterpret_cast<char*>(ws));
+        hipLaunchKernelGGL(gnca_ks_images, dim3(1), dim3(512), 0, st, ka, dst);
+        const int rc = check_launch();
+        if (rc != GNCA_OK) return rc;
+      }
       wimg = dst;
     }
   }
@@ -2097,9 +2101,12 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
   std::lock_guard<std::mutex> lk(ss->mu);
   hipStream_t sj[kRolloutSubs];
   for (int j = 0; j < nsub; ++j) sj[j] = j == 0 ? st : ss->s[j];
-  if (hipEventRecord(ss->fork, st) != hipSuccess) return GNCA_ERR_HIP;
-  for (int j = 1; j < nsub; ++j)
-    if (hipStreamWaitEvent(sj[j], ss->fork, 0) != hipSuccess) return GNCA_ERR_HIP;
+  // fork (not for a continuation piece: its sub-batch streams carry on from the previous piece)
+  if (!in0) {
+    if (hipEventRecord(ss->fork, st) != hipSuccess) return GNCA_ERR_HIP;
+    for (int j = 1; j < nsub; ++j)
+      if (hipStreamWaitEvent(sj[j], ss->fork, 0) != hipSuccess) return GNCA_ERR_HIP;
+  }
   char* wsb = reinterpret_cast<char*>(ws);
   int rc = GNCA_OK;
   for (int t = 0; t < steps && rc == GNCA_OK; ++t) {
@@ -2114,8 +2121,9 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
                      stamps ? stamps + ((size_t)t * nsub + j) * 4 * stamp_cap : nullptr, stamp_cap, wimg);
     }
   }
-  // join (also after a failed launch: the helper streams' work stays ordered before the caller's)
-  for (int j = 1; j < nsub; ++j) {
+  // join (also after a failed launch: the helper streams' work stays ordered before the caller's);
+  // not when another piece follows (ALIVE_OUT): the last piece joins
+  for (int j = 1; j < nsub && (!out_last || rc != GNCA_OK); ++j) {
     if (hipEventRecord(ss->join[j], sj[j]) != hipSuccess || hipStreamWaitEvent(st, ss->join[j], 0) != hipSuccess)
       return GNCA_ERR_HIP;
   }

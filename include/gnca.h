@@ -201,6 +201,10 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
  *   GNCA_ROLLOUT_ALIVE_IN   the first step's K1 reads them from `ws` (written by the previous call
  *                           with ALIVE_OUT on the same workspace; x = that call's x_final)
  * Both need 0 <= alpha_thr <= graph_alpha_thr (else GNCA_ERR_INVALID).  flags = 0 is gnca_rollout_f32.
+ * A rollout that runs as concurrent sub-batches (gnca_rollout_f32) forks its helper streams in the
+ * first piece and joins them into `stream` in the last one (the piece without ALIVE_OUT): between
+ * pieces, x_final is complete on `stream` only for sub-batch 0, so the caller must not read it
+ * before the last piece; continuation pieces reuse the first piece's weight images in `ws`.
  */
 #define GNCA_ROLLOUT_ALIVE_IN  (1u << 0)
 #define GNCA_ROLLOUT_ALIVE_OUT (1u << 1)
