@@ -74,9 +74,11 @@ def flop_per_cell(wl):
 
 
 def pmc_traffic(kernel):
+    """HBM bytes per STEP of ``kernel`` from the committed PMC passes: per-launch counter bytes x the
+    launches per step the passes ran with (sub-batches; rollout kernels of 2 half-batches)."""
     try:
-        d = json.load(open(PMC_TRAFFIC))["kernels"][kernel]
-        return d["traffic_bytes"]
+        d = json.load(open(PMC_TRAFFIC))
+        return d["kernels"][kernel]["traffic_bytes"] * d.get("launches_per_step", 1)
     except Exception:
         return None
 
@@ -694,7 +696,8 @@ def main():
             "dense_flop_per_launch": dense_flops, "live_flop_per_launch": live_flops,
             "live_fraction": live_frac,
             "traffic": pmc_traffic("K1") if headline else None,
-            "traffic_unit": f"bytes/launch (2*FETCH_SIZE+WRITE_SIZE, {os.path.relpath(PMC_TRAFFIC, ROOT)})",
+            "traffic_unit": f"HBM bytes per step (2*FETCH_SIZE+WRITE_SIZE summed over the step's K1 "
+                            f"launches, {os.path.relpath(PMC_TRAFFIC, ROOT)})",
             "k1_ms": k1_ms,
             "k1_ms_source": "per-workgroup s_memrealtime stamps (first instruction .. after the last "
                             "barrier, max - min over the launch's workgroups) in an identical re-run of "
@@ -703,11 +706,11 @@ def main():
             "mfma_pipe_note": "executed MFMA FLOPs in the MFMA's dtype (32-cell groups, padding "
                               "included) / that dtype's dense peak",
             "mfma_busy_pmc": pmc_busy,
-            "k1_launches_timed": launches}
+            "k1_launches_timed": launches * nsub}
     roof_k2 = {"bound": "hbm", "kernel": "gnca_k2_finalize", "update_field": "compact" if compact else "dense",
                "achieved": k2_bytes / (k2_ms * 1e-3) / 1e9,
                "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": k2_bytes / (k2_ms * 1e-3) / PEAK_HBM,
-               "k2_ms": k2_ms, "bytes_per_launch": k2_bytes, "k2_launches_timed": launches,
+               "k2_ms": k2_ms, "bytes_per_step": k2_bytes, "k2_launches_timed": launches * nsub,
                "traffic": pmc_traffic("K2") if headline else None}
 
     if rank == 0:

@@ -24,6 +24,8 @@ for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.cs
         if k:
             vals[k][r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
 res = {"fetch_correction": 2.0,
+       # rollout launches of each kernel per CA step when the passes ran (2: the sub-batch pipeline)
+       "launches_per_step": int(os.environ.get("PMC_LAUNCHES_PER_STEP", "1")),
        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over "
                  "`python3 bench.py --steps 4 --warmup 1 --no-cpu` (tools/pmc.sh); "
                  "FETCH_SIZE x2 per tools/ubench/fetch_calib.hip",
