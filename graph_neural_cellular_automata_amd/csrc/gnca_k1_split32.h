@@ -33,6 +33,11 @@ struct KS32Layout {
   int sp_slot, lst_slot;                                         // bytes per prepared-tile slot
 };
 
+// channel-plane stride of the 32-channel kernel's staged region: at least one pad float (the zero
+// tap of the border perception), quads (16-byte LDS-DMA rows); no bank offset between planes (the
+// two lane halves' ds_read_b32 reads are separate LDS cycles), so the 26 x 32 region fits 160 KB
+__host__ __device__ constexpr int ks32_pstr(int rhw) { return (rhw + 1 + 3) & ~3; }
+
 template <int TH, int TW, int RY, int RX>
 __host__ __device__ constexpr KS32Layout ks32_layout() {
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
@@ -40,7 +45,7 @@ __host__ __device__ constexpr KS32Layout ks32_layout() {
   int o = 0;
   L.sp_slot = ks_a16(RHW);
   L.lst_slot = ks_a16(TH * TW * 2);
-  L.xs = o; o += 16 * ks_pstr(RHW) * 4;           // one phase's 16 channel planes
+  L.xs = o; o += 16 * ks32_pstr(RHW) * 4;         // one phase's 16 channel planes
   L.sp = o; o += 2 * L.sp_slot;                   // sender plane (bytes 0/1), two slots
   L.ab = o; o += ks_a16(RHW);                     // the preparer's alive bytes over the region
   L.lst = o; o += 2 * L.lst_slot;                 // live-cell list, two slots
@@ -60,8 +65,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_b[];
   constexpr int C = 32, HD = 128, NT = 512, NW = 8;
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
-  constexpr int PSTR = ks_pstr(RHW);
-  constexpr int NI = (RHW + 63) / 64;
+  constexpr int PSTR = ks32_pstr(RHW);
+  constexpr int NQ = RHW / 4, NI4 = (NQ + 63) / 64;   // 16-byte quads of a channel plane
+  static_assert(RW % 4 == 0 && RX % 4 == 0 && TW % 4 == 0, "16-byte staging rows");
   constexpr int NCELL = TH * TW;
   constexpr KS32Layout L = ks32_layout<TH, TW, RY, RX>();
   static_assert(NCELL <= 32 * NW, "one 32-cell group per wave");
@@ -100,7 +106,8 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     return t;
   };
 
-  // channel planes [16ph, 16ph + 16) of tile t's (RH x RW) region -> xs (torus-wrapped), dword DMA
+  // channel planes [16ph, 16ph + 16) of tile t's (RH x RW) region -> xs (torus-wrapped), 16-byte
+  // LDS-DMA quads (RX, TW multiples of 4 and W % 4 == 0: a quad never straddles the wrap), quad
   // blocks w0, w0 + wstep, ...
   auto stage = [&](int t, int ph, int w0, int wstep) {
     const int b = t / a.tps, tin = t - b * a.tps;
@@ -108,19 +115,19 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     const int i0 = ty * TH, j0 = tx * TW;
     const float* xb = a.x + (size_t)b * C * HW;
 #pragma unroll 1
-    for (int ii_ = w0; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI); ii_ += wstep) {
-      const int e = 64 * ii_ + lane;
-      if (e < RHW) {   // lanes past the region masked off: the plane pads (zero taps) stay zero
-        const int vr = e / RW, vc = e - (e / RW) * RW;
+    for (int ii_ = w0; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI4); ii_ += wstep) {
+      const int q = 64 * ii_ + lane;
+      if (q < NQ) {   // lanes past the region masked off: the plane pads (zero taps) stay zero
+        const int e = 4 * q, vr = e / RW, vc = e - (e / RW) * RW;
         int ii = i0 - RY + vr, jj = j0 - RX + vc;
         ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
         jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
         const float* src0 = xb + (size_t)(16 * ph) * HW + ii * W + jj;
-        float* dst = xs + 64 * ii_;
+        float* dst = xs + 256 * ii_;
 #pragma unroll 4
         for (int c = 0; c < 16; ++c)
           __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (size_t)c * HW),
-                                           (__attribute__((address_space(3))) void*)(dst + c * PSTR), 4, 0, 0);
+                                           (__attribute__((address_space(3))) void*)(dst + c * PSTR), 16, 0, 0);
       }
     }
   };

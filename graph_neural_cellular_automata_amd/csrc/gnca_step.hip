@@ -1357,8 +1357,8 @@ static const Variant kVariants[] = {
     GNCA_SV(8, 20, 1, 4, 0),
     // 32 channels (BASELINE config 5: 128^2, r = 5, K = 16): 16x16 tiles, channel planes staged
     // in two 16-channel phases (gnca_k1_split32.h); graph and no-message steps
-    GNCA_S32V(16, 16, 5, 5, 16),
-    GNCA_S32V(16, 16, 1, 1, 0),
+    GNCA_S32V(16, 16, 5, 8, 16),   // RX 8 (not 5): quad-aligned 16-byte LDS-DMA rows
+    GNCA_S32V(16, 16, 1, 4, 0),
     // runtime geometry: every other shape class
     GNCA_GV(4, 32),   GNCA_GV(4, 64),   GNCA_GV(4, 128),  GNCA_GV(8, 32),   GNCA_GV(8, 64),
     GNCA_GV(8, 128),  GNCA_GV(12, 64),  GNCA_GV(12, 128), GNCA_GV(16, 32),  GNCA_GV(16, 64),
