@@ -144,7 +144,7 @@ def test_k1_variant_names(lib):
     assert name(1024, 16, 72, r4) == ("gnca_k1_split<24,36,4,4,8>", "bf16x6")
     assert name(8, 16, 72, r4) == ("gnca_k1_split<8,24,4,4,8>", "bf16x6")
     assert name(8, 16, 72, [], graph=False) == ("gnca_k1_split<8,24,1,4,0>", "bf16x6")
-    assert name(128, 32, 128, r5) == ("gnca_k1_split32<16,16,5,5,16>", "bf16x6")
+    assert name(128, 32, 128, r5) == ("gnca_k1_split32<16,16,5,8,16>", "bf16x6")
     # the rollout's compact update field: large batches on the bf16-split K1s only
     comp = lambda B, C, H, offs, graph=True: S.rollout_compact(S.make_desc(
         B=B, C=C, H=H, W=H, hidden=128, d_model=16, offsets=offs,

@@ -29,7 +29,7 @@ CASES = {
                           "gnca_k1_split<8,24,1,4,0>"),
     # BASELINE config 5's shape class: 32 ch, 128^2, r=5, K=16 (48 steps: the f64 oracle's time)
     "c5_split32": ("graph_torus_c32_r5_k16_b1_48", True, 32, 128, 8, 5, 16, 48, (0, 7),
-                   "gnca_k1_split32<16,16,5,5,16>"),
+                   "gnca_k1_split32<16,16,5,8,16>"),
 }
 GAIN, THR, MSG, FIRE, SEED = 0.05, 0.12, 0.25, 0.5, 5
 
