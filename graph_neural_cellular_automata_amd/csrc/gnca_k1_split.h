@@ -252,7 +252,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   constexpr KSLayout L = ks_layout<TH, TW, RY, RX>();
   static_assert(RW % 4 == 0 && RX % 4 == 0 && TW % 4 == 0, "16-byte staging rows");
   static_assert(RY >= 1 && RX >= 1, "perception halo");
-  static_assert(L.total <= 160 * 1024, "LDS");
+  static_assert(L.total + 512 <= 160 * 1024, "LDS (+ the compiler's static LDS, e.g. __syncthreads_and)");
   static_assert(7 * PSTR * 4 + 4 * RHW < 65536, "channel offsets fit the DS immediate");
   static_assert(TW <= 64, "one ballot per tile row (compact update field)");
   constexpr bool GRAPH = KU > 0;

@@ -44,11 +44,11 @@ __host__ __device__ constexpr KS32Layout ks32_layout() {
   KS32Layout L{};
   int o = 0;
   L.sp_slot = ks_a16(RHW);
-  L.lst_slot = ks_a16(TH * TW * 2);
+  L.lst_slot = ks_a16(TH * TW);   // u8 cell indices (TH * TW <= 256)
   L.xs = o; o += 16 * ks32_pstr(RHW) * 4;         // one phase's 16 channel planes
   L.sp = o; o += 2 * L.sp_slot;                   // sender plane (bytes 0/1), two slots
   L.ab = o; o += ks_a16(RHW);                     // the preparer's alive bytes over the region
-  L.lst = o; o += 2 * L.lst_slot;                 // live-cell list, two slots
+  L.lst = o; o += 2 * L.lst_slot;                 // live-cell list (u8), two slots
   L.cnt = o; o += 16;                             // live cells per slot; staged-reads-done counter
   L.cb = o; o += ks_a16(8 * (TH * TW / 64 + 2));  // the preparer's 64-cell chunk ballots
   L.w1 = o; o += 4 * 3 * 2 * 3 * 1024;            // [rb][f][p][part][lane] x 16 B
@@ -72,7 +72,8 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   constexpr KS32Layout L = ks32_layout<TH, TW, RY, RX>();
   static_assert(NCELL <= 32 * NW, "one 32-cell group per wave");
   static_assert(RY >= 1 && RX >= 1, "perception halo");
-  static_assert(L.total <= 160 * 1024, "LDS");
+  static_assert(L.total + 512 <= 160 * 1024, "LDS (+ the compiler's static LDS, e.g. __syncthreads_and)");
+  static_assert(NCELL <= 256, "u8 live-cell indices");
   static_assert(7 * PSTR * 4 + 4 * RHW < 65536, "channel offsets fit the DS immediate");
   constexpr bool GRAPH = KU > 0;
   constexpr int PW = NW - 1;   // the preparer / next-tile stager (no group unless > 224 live cells)
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     const int i0 = ty * TH, j0 = tx * TW;
     const size_t cell0 = (size_t)i0 * W + j0;
     uint8_t* spp = reinterpret_cast<uint8_t*>(smem_b + L.sp + s * L.sp_slot);
-    uint16_t* lstp = reinterpret_cast<uint16_t*>(smem_b + L.lst + s * L.lst_slot);
+    uint8_t* lstp = reinterpret_cast<uint8_t*>(smem_b + L.lst + s * L.lst_slot);
     uint8_t* abq = reinterpret_cast<uint8_t*>(smem_b + L.ab);
     uint64_t* cb = reinterpret_cast<uint64_t*>(smem_b + L.cb);
     {
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       if (lane == 0) cb[n0 >> 6] = bal;
       if (compact && inb && tj == 0) a.rpre[(size_t)t * TH + ti] = (uint32_t)(nl + pre);
       if (live) {
-        lstp[nl + pre] = (uint16_t)n;
+        lstp[nl + pre] = (uint8_t)n;
       } else if (inb && !compact) {   // (compact: K2 masks the alpha plane by the row tables)
         float* oz = outb + (size_t)ti * W + tj;
 #pragma unroll
@@ -306,7 +307,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     const size_t cell0 = (size_t)i0 * W + j0;
     float* outb = a.out + (size_t)b * C * HW + cell0;
     const uint8_t* sp = reinterpret_cast<const uint8_t*>(smem_b + L.sp + par * L.sp_slot);
-    const uint16_t* lst = reinterpret_cast<const uint16_t*>(smem_b + L.lst + par * L.lst_slot);
+    const uint8_t* lst = reinterpret_cast<const uint8_t*>(smem_b + L.lst + par * L.lst_slot);
     const int nlive = cnt[par];
     if (wave == PW && nxt < t_end) prep(nxt, par ^ 1);
 
