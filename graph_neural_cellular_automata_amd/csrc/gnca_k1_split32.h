@@ -28,6 +28,10 @@
 
 namespace gnca {
 
+#ifndef GNCA_S32_STAGERS
+#define GNCA_S32_STAGERS 1   // the next tile's phase-0 DMA split over the waves without a group (0: the preparer alone)
+#endif
+
 struct KS32Layout {
   int xs, sp, ab, lst, cnt, cb, w1, bias, w2, wm, bml, total;   // byte offsets
   int sp_slot, lst_slot;                                         // bytes per prepared-tile slot
@@ -109,24 +113,29 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
 
   // channel planes [16ph, 16ph + 16) of tile t's (RH x RW) region -> xs (torus-wrapped), 16-byte
   // LDS-DMA quads (RX, TW multiples of 4 and W % 4 == 0: a quad never straddles the wrap), quad
-  // blocks w0, w0 + wstep, ...
+  // items w0, w0 + wstep, ... of (quad block, channel slice): with more waves than quad blocks the
+  // 16 channels are sliced so every wave issues a share (8 waves, 4 blocks: 8 instructions each)
   auto stage = [&](int t, int ph, int w0, int wstep) {
     const int b = t / a.tps, tin = t - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
     const float* xb = a.x + (size_t)b * C * HW;
+    int cs = 1;
+    while (cs < 16 && wstep >= 2 * cs * NI4) cs *= 2;
+    const int cn = 16 / cs;
 #pragma unroll 1
-    for (int ii_ = w0; ii_ < ((GNCA_ABLATE & kAblStage) ? 0 : NI4); ii_ += wstep) {
+    for (int it = w0; it < ((GNCA_ABLATE & kAblStage) ? 0 : NI4 * cs); it += wstep) {
+      const int ii_ = it % NI4, c0 = (it / NI4) * cn;
       const int q = 64 * ii_ + lane;
       if (q < NQ) {   // lanes past the region masked off: the plane pads (zero taps) stay zero
         const int e = 4 * q, vr = e / RW, vc = e - (e / RW) * RW;
         int ii = i0 - RY + vr, jj = j0 - RX + vc;
         ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
         jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-        const float* src0 = xb + (size_t)(16 * ph) * HW + ii * W + jj;
-        float* dst = xs + 256 * ii_;
+        const float* src0 = xb + (size_t)(16 * ph + c0) * HW + ii * W + jj;
+        float* dst = xs + 256 * ii_ + c0 * PSTR;
 #pragma unroll 4
-        for (int c = 0; c < 16; ++c)
+        for (int c = 0; c < cn; ++c)
           __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (size_t)c * HW),
                                            (__attribute__((address_space(3))) void*)(dst + c * PSTR), 16, 0, 0);
       }
@@ -431,10 +440,20 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     // phase-1 reads (release / acquire on the LDS counter), under the groups' MFMAs
     const int ngrp = (nlive + 31) >> 5;
     if (has) __hip_atomic_fetch_add(xsd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (wave == PW && nxt < t_end) {
+    // stagers: every wave without a group (waves ngrp..7, the preparer among them), or the preparer
+    // alone when all 8 waves have one; the 208 LDS-DMA instructions of a phase issued by one wave
+    // take longer than the groups' MFMAs (~60-100 cycles each beside MFMAs)
+#if GNCA_S32_STAGERS
+    const int nst = ngrp < NW ? NW - ngrp : 1;
+    const bool stager = ngrp < NW ? wave >= ngrp : wave == PW;
+#else
+    const int nst = 1;
+    const bool stager = wave == PW;
+#endif
+    if (stager && nxt < t_end) {
       while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xbase < ngrp)
         __builtin_amdgcn_s_sleep(1);
-      stage(nxt, 0, 0, 1);
+      stage(nxt, 0, nst > 1 ? wave - ngrp : 0, nst);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     xbase += ngrp;
