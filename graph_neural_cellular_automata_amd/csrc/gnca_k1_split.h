@@ -599,6 +599,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       split3_x8(y2, yf[2][0], yf[2][1], yf[2][2]);
       // this group's reads of the staged planes are done (release: they stay before the count)
       __hip_atomic_fetch_add(xsd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      PROF_MARK(2);   // pull + gather + perception + splits
       if (GNCA_ABLATE & kAblMfma) {
 #pragma unroll
         for (int kc = 0; kc < 3; ++kc) asm volatile("" ::"v"(yf[kc][0]), "v"(yf[kc][1]), "v"(yf[kc][2]));
@@ -786,6 +787,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
           pg[2 * q + 1] = d2;
         }
       }
+      PROF_MARK(4);   // MFMAs + epilogue + partials
     }
 
     PROF_MARK(4);   // group loop

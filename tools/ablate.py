@@ -38,7 +38,7 @@ def build():
             continue
         flags = (["-DGNCA_PROFILE"] if bits is None else
                  bits.split() if isinstance(bits, str) else [f"-DGNCA_ABLATE={bits}"])
-        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize",
                *flags, f"-I{ROOT}/include", src, "-o", os.path.join(OUT, f"lib_{name}.so")]
         procs.append(subprocess.Popen(cmd, stderr=subprocess.DEVNULL))
         if len(procs) >= 4:
@@ -115,7 +115,7 @@ def run(reps=15, rounds=3):
     full = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16).astype(np.float64)
     ws = full[:, 8:].sum() > 0
     if os.environ.get("ABLATE_PROF_SETS") == "w03":   # the split K1: wave 0 and the preparer wave 3
-        names = ["dma_issue", "dma_wait+barrier", "-", "preparer", "groups", "partial_bins",
+        names = ["dma_issue", "dma_wait+barrier", "gather+perc", "preparer", "group_mfma+epi", "partial_bins",
                  "barrier_after_groups", "loop_top"]
         sets = [("wave 0 (SIMD 0, older)", names, full[:, :8]),
                 ("wave 3 (SIMD 3, preparer)", names, full[:, 8:])]
