@@ -86,6 +86,68 @@ __device__ __forceinline__ f32x16 mfma_bx(u32x4 a, u32x4 b, f32x16 c) {
                                                  c, 0, 0, 0);
 }
 
+#ifndef GNCA_K1_PIPE_LDS
+#define GNCA_K1_PIPE_LDS 1   // pipeline depth of the gather / perception reads (A/B builds: 0 = the plain loops)
+#endif
+
+// Gather of alive-masked x over the KU offsets for one lane's 8 channels (plane stride PSTR), software-
+// pipelined: the 9 LDS reads of offset o + 1 are issued before the FMAs of offset o (sched_barrier
+// fences keep the order), so reads are always in flight.  Left to itself the compiler emitted read /
+// wait / FMA chains (a wave alone on its SIMD then pays every LDS latency: 32-channel K1, ~2/3 of
+// each phase).  Same FMA order as the plain loop: bitwise the same sums.
+template <int KU, int PSTR>
+__device__ __forceinline__ void ks_gather8(const int* odl, const float* xq, const uint8_t* spq, float (&gv)[8],
+                                           float& S) {
+  constexpr int D = GNCA_K1_PIPE_LDS;   // offsets whose reads are in flight ahead of the FMAs
+  float xv[D + 1][8];
+  uint32_t sv[D + 1];
+  auto ld = [&](int o) {
+    const int d = odl[o];
+    sv[o % (D + 1)] = spq[-d];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[o % (D + 1)][j] = xq[j * PSTR - d];
+  };
+#pragma unroll
+  for (int o = 0; o < D && o < KU; ++o) ld(o);
+#pragma unroll
+  for (int o = 0; o < KU; ++o) {
+    if (o + D < KU) ld(o + D);
+    __builtin_amdgcn_sched_barrier(0);
+    const float s_ = (float)sv[o % (D + 1)];
+    S += s_;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gv[j] = fmaf(s_, xv[o % (D + 1)][j], gv[j]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// The frozen Sobel bank's perception of one lane's 8 channels from the 9 tap offsets t[] (zero taps at
+// the image border), pipelined as ks_gather8: channel j + 1's 9 reads in flight under channel j's
+// arithmetic.  y0 = identity, y1 = Sobel-x, y2 = Sobel-y with shared diagonal differences.
+template <int PSTR>
+__device__ __forceinline__ void ks_sobel8(const float* xs, const int (&t)[9], float (&y0)[8], float (&y1)[8],
+                                          float (&y2)[8]) {
+  constexpr int D = GNCA_K1_PIPE_LDS;
+  float nv[D + 1][9];
+  auto ld = [&](int j) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) nv[j % (D + 1)][k] = xs[t[k] + j * PSTR];
+  };
+#pragma unroll
+  for (int j = 0; j < D; ++j) ld(j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (j + D < 8) ld(j + D);
+    __builtin_amdgcn_sched_barrier(0);
+    const float* n = nv[j % (D + 1)];
+    y0[j] = n[4];
+    const float dg = n[0] - n[8], da = n[2] - n[6];
+    y1[j] = fmaf(2.f, n[3] - n[5], dg - da);
+    y2[j] = fmaf(2.f, n[1] - n[7], dg + da);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // channel-plane stride (floats) of the split kernel's staged region: at least one pad float
 // (the zero tap of the border perception), 16 mod 32 (planes start 16 banks apart), quads
 __host__ __device__ constexpr int ks_pstr(int rhw) {
@@ -138,7 +200,7 @@ template <int NT, bool GRAPH, bool TO_LDS>
 __device__ __forceinline__ void ks_fill_images(const K1Args& a, char* dst, int tid);
 
 #ifndef GNCA_K1_LEAN
-#define GNCA_K1_LEAN 1   // register-lean group body (one GEMM2 accumulator seeded with the message,
+#define GNCA_K1_LEAN 2   // 2: the lean body as a software pipeline over the row blocks; 1: register-lean group body (one GEMM2 accumulator seeded with the message,
                          // GEMM1 row blocks double-buffered through GEMM2); 0: round 2's body
 #endif
 
@@ -236,6 +298,18 @@ __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst)
 #define GNCA_K1_PRIO 2   // wave issue priority of K1 (s_setprio): > 0 favours K1 over a co-resident K2
 #endif
 
+#ifndef GNCA_PREP_PRIO
+#define GNCA_PREP_PRIO 3   // the preparer's issue priority while it prepares (K1 0.397 -> 0.384 ms; 0: unchanged)
+#endif
+
+#ifndef GNCA_K1_STAGGER
+#define GNCA_K1_STAGGER 0   // A/B builds: waves 4-7 (the younger of each SIMD) sleep 64 x N cycles before their first pull of a tile
+#endif
+
+#ifndef GNCA_K1_DYNPRIO
+#define GNCA_K1_DYNPRIO 0   // A/B builds: a wave raises its issue priority by this much over its group's MFMA section
+#endif
+
 #ifndef GNCA_DMA_WAVES
 #define GNCA_DMA_WAVES 1   // A/B builds: waves (the first failing pulls) sharing the next tile's DMA (3: K1 0.4015-0.4044 vs 0.4008-0.4026 ms with 1)
 #endif
@@ -328,6 +402,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   // the dead cells' zeros go to global memory.  The pre-update masks are the alive bytes (K2's
   // hand-over in a rollout, else gnca_k_alive over this step's alpha plane).
   auto prep = [&](int t, int s) {
+    if (GNCA_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_PREP_PRIO);
     const int b = t / a.tps, tin = t - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
@@ -408,6 +483,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       }
     }
     if (lane == 0) cnt[s] = nl;
+    if (GNCA_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO);
   };
 
   PROF_DECL
@@ -495,6 +571,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const bool img_top = i0 == 0, img_bot = i0 + TH == H, img_lft = j0 == 0, img_rgt = j0 + TW == W;
     // (every lane adds 1: the wave's 64 increments are one LDS instruction, so the counter moves by
     //  64 per pull and any lane's old value >> 6 is the pulled group)
+    if (GNCA_K1_STAGGER > 0 && wave >= 4) __builtin_amdgcn_s_sleep(GNCA_K1_STAGGER);
     int q = pull();
 #pragma unroll 1
     for (; q < qend; q = pull()) {
@@ -518,18 +595,22 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         for (int j = 0; j < 8; ++j) gv[j] = 0.f;
         const float* xq = xs + hb + pidx;
         const uint8_t* spq = sp + pidx;
+        if (GNCA_K1_PIPE_LDS && !(GNCA_ABLATE & 4096)) {
+          ks_gather8<KU, PSTR>(a.odl, xq, spq, gv, S);
+        } else {
 #pragma unroll
-        for (int o = 0; o < KU; ++o) {
-          const int d = a.odl[o];
-          const float s_ = (float)spq[-d];
-          S += s_;
-          const float* xo = xq - d;
+          for (int o = 0; o < KU; ++o) {
+            const int d = a.odl[o];
+            const float s_ = (float)spq[-d];
+            S += s_;
+            const float* xo = xq - d;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            // (GNCA_ABLATE & 4096: timing only, one channel's read stands in for all eight)
-            float xv_ = xo[(GNCA_ABLATE & 4096) ? 0 : j * PSTR];
-            if (GNCA_ABLATE & 4096) asm volatile("" : "+v"(xv_));
-            gv[j] = fmaf(s_, xv_, gv[j]);
+            for (int j = 0; j < 8; ++j) {
+              // (GNCA_ABLATE & 4096: timing only, one channel's read stands in for all eight)
+              float xv_ = xo[(GNCA_ABLATE & 4096) ? 0 : j * PSTR];
+              if (GNCA_ABLATE & 4096) asm volatile("" : "+v"(xv_));
+              gv[j] = fmaf(s_, xv_, gv[j]);
+            }
           }
         }
         const float wu = a.uniform_w;
@@ -557,6 +638,9 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         if (GNCA_ABLATE & kAblPerceive) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) y0[j] = y1[j] = y2[j] = 0.f;
+        } else if (sobel && GNCA_K1_PIPE_LDS && !(GNCA_ABLATE & 4096)) {
+          const int tt[9] = {t0, t1, t2, t3, bc, t5, t6, t7, t8};
+          ks_sobel8<PSTR>(xs, tt, y0, y1, y2);
         } else if (sobel) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -600,12 +684,115 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       // this group's reads of the staged planes are done (release: they stay before the count)
       __hip_atomic_fetch_add(xsd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       PROF_MARK(2);   // pull + gather + perception + splits
+      if (GNCA_K1_DYNPRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO + GNCA_K1_DYNPRIO);
       if (GNCA_ABLATE & kAblMfma) {
 #pragma unroll
         for (int kc = 0; kc < 3; ++kc) asm volatile("" ::"v"(yf[kc][0]), "v"(yf[kc][1]), "v"(yf[kc][2]));
       }
 
 #if GNCA_K1_LEAN
+#if GNCA_K1_LEAN >= 2
+      // -- The group's GEMMs as a software pipeline over the row blocks: stage rb issues row block
+      //    rb + 1's GEMM1 chain (bias + 18 products into acc1[(rb + 1) & 1]) two MFMAs at a time,
+      //    each pair fenced together with one piece of row block rb's ReLU / split VALU, then rb's two
+      //    GEMM2 k-chunks.  Left alone the scheduler issued each row block's 19 MFMAs back to back and
+      //    then its ~104 split VALU with the matrix pipe idle; here the VALU sits in the MFMA shadows.
+      //    The message MFMAs and GEMM1 of row block 0 carry the message tanh the same way.  Every
+      //    accumulation chain keeps its order: bitwise the results of the plain body. --
+      f32x16 acc2 = {};
+      f32x16 acc1[2];
+      // GEMM1 product q (0..17) of one row block: k-chunk q / 6, (A part, B part) by q % 6
+      auto g1p = [&](f32x16& ac, const u32x4 (&A)[3][3], int q) {
+        const int kc = q / 6, pp = q % 6;
+        const int ap = (pp == 2 || pp == 5) ? 1 : (pp == 4 ? 2 : 0);
+        const int bp = (pp == 1 || pp == 5) ? 1 : (pp == 3 ? 2 : 0);
+        ac = mfma_bx(A[kc][ap], yf[kc][bp], ac);
+      };
+      auto ldA = [&](int rb, u32x4 (&A)[3][3], u32x4& bz) {
+        bz = *reinterpret_cast<const u32x4*>(smem_b + L.bias + rb * 512 + r32 * 16);
+#pragma unroll
+        for (int kc = 0; kc < 3; ++kc)
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt)
+            A[kc][pt] = *reinterpret_cast<const u32x4*>(smem_b + L.w1 + (rb * 3 + kc) * 1024 + lane * 16 + pt * 12288);
+      };
+      {
+        u32x4 A[3][3], bz;
+        ldA(0, A, bz);
+        f32x16 accm = {};
+        if constexpr (GRAPH) {
+          const u32x4 wmA = *reinterpret_cast<const u32x4*>(smem_b + wmA_o);
+          const u32x4 wmB = *reinterpret_cast<const u32x4*>(smem_b + wmB_o);
+          const u32x4 wmC = *reinterpret_cast<const u32x4*>(smem_b + wmC_o);
+          accm = mfma_bx(wmA, g0, accm);
+          accm = mfma_bx(wmB, g0, accm);
+          accm = mfma_bx(wmA, g1, accm);
+          accm = mfma_bx(wmC, g2, accm);
+        }
+        acc1[0] = mfma_bx(bz, ones, f32x16{});
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          g1p(acc1[0], A, 2 * k);
+          g1p(acc1[0], A, 2 * k + 1);
+          if constexpr (GRAPH) {
+            if (k < 4) {
+#pragma unroll
+              for (int r = 2 * k; r < 2 * k + 2; ++r) {
+                const float bm_ = reinterpret_cast<const float*>(smem_b + bml_o)[r];
+                acc2[r] = fast_tanh(fmaf(bm_, S, accm[r] + accm[r + 8])) * ((hz && r < 4) ? 0.f : mgain);
+              }
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        f32x16& cur = acc1[rb & 1];
+        f32x16& nx = acc1[(rb + 1) & 1];
+        const bool more = rb < 3;
+        u32x4 A[3][3], bz;
+        if (more) ldA(rb + 1, A, bz);
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const int s = 2 * rb + ss;
+          const u32x4 T0 = *reinterpret_cast<const u32x4*>(smem_b + w2T0 + s * 512);
+          const u32x4 T1 = *reinterpret_cast<const u32x4*>(smem_b + w2T1 + s * 512);
+          float hv[8];
+          // step: ReLU of this k-chunk (+ the bias MFMA of the next row block, first chunk)
+          if (more && ss == 0) nx = mfma_bx(bz, ones, f32x16{});
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hv[j] = relu_nan(cur[8 * ss + j]);
+          __builtin_amdgcn_sched_barrier(0);
+          // four steps: two GEMM1 products of the next row block + one split pair
+          u32x4 h0, h1, h2;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (more) {
+              g1p(nx, A, 8 * ss + 2 * k);
+              g1p(nx, A, 8 * ss + 2 * k + 1);
+            }
+            uint32_t p0, p1, p2;
+            split3_pair(hv[2 * k], hv[2 * k + 1], p0, p1, p2);
+            h0[k] = p0;
+            h1[k] = p1;
+            h2[k] = p2;
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          // step: this k-chunk's GEMM2 products (+ the next row block's last two, second chunk)
+          if (more && ss == 1) {
+            g1p(nx, A, 16);
+            g1p(nx, A, 17);
+          }
+          acc2 = mfma_bx(T0, h0, acc2);
+          acc2 = mfma_bx(T1, h0, acc2);
+          acc2 = mfma_bx(T0, h1, acc2);
+          acc2 = mfma_bx(T0, h2, acc2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#else   // GNCA_K1_LEAN == 1
       // -- message: M = WM.G (stacks [M0;M1] G0 + [M2;0] G0 + [M0;M1] G1 + [M0;0] G2), then the
       //    message term tanh(M + bm S) * gain seeds GEMM2's accumulator (top half; bottom 0) --
       f32x16 acc2 = {};
@@ -674,6 +861,8 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
           acc2 = mfma_bx(T0, h2, acc2);
         }
       }
+
+#endif   // GNCA_K1_LEAN >= 2
 
       // -- epilogue: dx = dl + tanh(m) * gain (already in acc2's top half) for channels
       //    c = (r&3) + 8(r>>2) + 4h; the keep mask is the live list itself --
@@ -788,6 +977,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         }
       }
       PROF_MARK(4);   // MFMAs + epilogue + partials
+      if (GNCA_K1_DYNPRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO);
     }
 
     PROF_MARK(4);   // group loop

@@ -28,6 +28,16 @@
 
 namespace gnca {
 
+#ifndef GNCA_S32_PREP_PRIO
+#define GNCA_S32_PREP_PRIO 3
+#endif
+
+#ifndef GNCA_S32_LATE_PREP
+#define GNCA_S32_LATE_PREP 0   // the preparer builds the next tile's slot after the phase-1 staging (under
+                               // the groups' phase-1 reads and MFMAs) instead of beside phase 0, and
+                               // leaves the next tile's phase-0 DMA to the other waves without a group
+#endif
+
 #ifndef GNCA_S32_STAGERS
 #define GNCA_S32_STAGERS 1   // the next tile's phase-0 DMA split over the waves without a group (0: the preparer alone)
 #endif
@@ -146,6 +156,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   // live-cell list into slot s, the compact field's row tables (and, dense field, the dead cells'
   // zeros).  The pre-update masks are the alive bytes (the previous K2's, or gnca_k_alive's).
   auto prep = [&](int t, int s) {
+    // the preparer (the younger wave of its SIMD, beside a group wave) at the top issue priority
+    // while it prepares: it is on the tile's critical path (c5 K1 0.559 -> 0.534 ms)
+    if (GNCA_S32_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_S32_PREP_PRIO);
     const int b = t / a.tps, tin = t - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
@@ -157,25 +170,30 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     {
       const uint8_t* alb = a.alive + (size_t)b * HW;
       constexpr int NU = (RHW + 63) / 64;
-      uint32_t v[NU];
+      // (late prep: NB loads in flight per batch, few registers beside the held phase-0 fragments)
+      constexpr int NB = GNCA_S32_LATE_PREP ? 4 : NU;
+#pragma unroll 1
+      for (int u0 = 0; u0 < NU; u0 += NB) {
+        uint32_t v[NB];
 #pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        const int e = 64 * u + lane;
-        v[u] = 0u;
-        if (e < RHW) {
-          const int vr = e / RW, vc = e - (e / RW) * RW;
-          int ii = i0 - RY + vr, jj = j0 - RX + vc;
-          ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
-          jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-          v[u] = alb[ii * W + jj];
+        for (int u = 0; u < NB; ++u) {
+          const int e = 64 * (u0 + u) + lane;
+          v[u] = 0u;
+          if (u0 + u < NU && e < RHW) {
+            const int vr = e / RW, vc = e - (e / RW) * RW;
+            int ii = i0 - RY + vr, jj = j0 - RX + vc;
+            ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
+            jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
+            v[u] = alb[ii * W + jj];
+          }
         }
-      }
 #pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        const int e = 64 * u + lane;
-        if (e < RHW) {
-          abq[e] = (uint8_t)v[u];
-          if constexpr (GRAPH) spp[e] = a2a ? (uint8_t)((v[u] >> 1) & 1u) : (uint8_t)1;
+        for (int u = 0; u < NB; ++u) {
+          const int e = 64 * (u0 + u) + lane;
+          if (u0 + u < NU && e < RHW) {
+            abq[e] = (uint8_t)v[u];
+            if constexpr (GRAPH) spp[e] = a2a ? (uint8_t)((v[u] >> 1) & 1u) : (uint8_t)1;
+          }
         }
       }
     }
@@ -220,6 +238,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       }
     }
     if (lane == 0) cnt[s] = nl;
+    if (GNCA_S32_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(0);
   };
 
   // prologue: the first tile's phase-0 DMA and planes, then the weight images
@@ -307,8 +326,10 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   const float mgain = GRAPH ? a.message_gain : 0.f;
   const bool hz = hidden_only && h == 0;   // channels (r&3) + 4h < 4 (r < 4) are the RGBA ones
 
+  PROF_DECL
   int par = 0;
   while (tile < t_end) {
+    PROF_MARK(7);   // loop top
     const int nxt = next_active(tile + per_x);
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
@@ -318,7 +339,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     const uint8_t* sp = reinterpret_cast<const uint8_t*>(smem_b + L.sp + par * L.sp_slot);
     const uint8_t* lst = reinterpret_cast<const uint8_t*>(smem_b + L.lst + par * L.lst_slot);
     const int nlive = cnt[par];
-    if (wave == PW && nxt < t_end) prep(nxt, par ^ 1);
+    // (late prep: at the tile start only when the preparer has a group itself, > 224 live cells)
+    if (wave == PW && nxt < t_end && (!GNCA_S32_LATE_PREP || 32 * PW < nlive)) prep(nxt, par ^ 1);
+    PROF_MARK(0);   // preparer
 
     // ---- one 32-cell group per wave; its accumulators live across the two channel phases ----
     const bool has = 32 * wave < nlive;   // wave-uniform
@@ -337,10 +360,16 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
       if (ph == 1) {
+        PROF_MARK(1);   // phase 0: gather + perception
         __syncthreads();   // every wave is done with phase 0's planes
         stage(tile, 1, wave, NW);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        PROF_MARK(2);   // phase-1 staging (barrier, DMA, wait, barrier)
+        if (GNCA_S32_LATE_PREP && wave == PW && !has && nxt < t_end) {
+          prep(nxt, par ^ 1);
+          PROF_MARK(0);
+        }
       }
       if (!has) continue;
       // -- gather of alive-masked x, this phase's channels 16ph + 8h + j (uniform weight 1/k) --
@@ -352,15 +381,19 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
         const float* xq = xs + hb + pidx;
         const uint8_t* spq = sp + pidx;
         float Sp = 0.f;
+        if (GNCA_K1_PIPE_LDS) {
+          ks_gather8<KU, PSTR>(a.odl, xq, spq, gv, Sp);
+        } else {
 #pragma unroll
-        for (int o = 0; o < KU; ++o) {
-          const int d = a.odl[o];
-          const float s_ = (float)spq[-d];
-          Sp += s_;
-          const float* xo = xq - d;
+          for (int o = 0; o < KU; ++o) {
+            const int d = a.odl[o];
+            const float s_ = (float)spq[-d];
+            Sp += s_;
+            const float* xo = xq - d;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) gv[j] = fmaf(s_, xo[j * PSTR], gv[j]);
-          if ((o & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // <= 4 offsets' reads in flight
+            for (int j = 0; j < 8; ++j) gv[j] = fmaf(s_, xo[j * PSTR], gv[j]);
+            if ((o & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // <= 4 offsets' reads in flight
+          }
         }
         const float wu = a.uniform_w;
 #pragma unroll
@@ -389,6 +422,9 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       if (GNCA_ABLATE & kAblPerceive) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) y0[j] = y1[j] = y2[j] = 0.f;
+      } else if (sobel && GNCA_K1_PIPE_LDS) {
+        const int tt[9] = {t0, t1, t2, t3, bc, t5, t6, t7, t8};
+        ks_sobel8<PSTR>(xs, tt, y0, y1, y2);
       } else if (sobel) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -438,14 +474,17 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
 
     // the next tile's phase-0 planes, staged by the preparer as soon as every group is past its
     // phase-1 reads (release / acquire on the LDS counter), under the groups' MFMAs
+    PROF_MARK(3);   // phase 1: gather + perception
     const int ngrp = (nlive + 31) >> 5;
     if (has) __hip_atomic_fetch_add(xsd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     // stagers: every wave without a group (waves ngrp..7, the preparer among them), or the preparer
     // alone when all 8 waves have one; the 208 LDS-DMA instructions of a phase issued by one wave
     // take longer than the groups' MFMAs (~60-100 cycles each beside MFMAs)
 #if GNCA_S32_STAGERS
-    const int nst = ngrp < NW ? NW - ngrp : 1;
-    const bool stager = ngrp < NW ? wave >= ngrp : wave == PW;
+    // (late prep: the preparer stages only when it is the one wave without a group)
+    const int nidle = NW - ngrp - ((GNCA_S32_LATE_PREP && ngrp < NW - 1) ? 1 : 0);
+    const int nst = nidle > 0 ? nidle : 1;
+    const bool stager = nidle > 0 ? (wave >= ngrp && wave < ngrp + nidle) : wave == PW;
 #else
     const int nst = 1;
     const bool stager = wave == PW;
@@ -457,6 +496,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     xbase += ngrp;
+    PROF_MARK(4);   // next tile's phase-0 staging (stagers)
 
     float s1 = 0.f, s2 = 0.f;
     if (has && !(GNCA_ABLATE & kAblMfma)) {
@@ -551,6 +591,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       }
     }
 
+    PROF_MARK(5);   // MFMAs + epilogue
     // ---- per-(tile, wave) GroupNorm partials (fp64 wave shuffle; K2 sums them in fixed order) ----
     double d1 = s1, d2 = s2;
     for (int off = 32; off > 0; off >>= 1) {
@@ -562,9 +603,11 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
       a.stats[((size_t)tile * NW + wave) * 2 + 1] = d2;
     }
     __syncthreads();   // groups done; the next tile's phase 0 staged; slot par^1 ready
+    PROF_MARK(6);   // partials + tile barrier
     tile = nxt;
     par ^= 1;
   }
+  PROF_STORE_W07;
   GNCA_STAMP_END(a.stamps);
 }
 

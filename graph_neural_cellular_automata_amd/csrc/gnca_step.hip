@@ -74,7 +74,10 @@ __device__ unsigned long long g_prof[1024][2 * kProfPhases];   // [.][8..15]: sp
 #define PROF_STORE_W04 do { if ((threadIdx.x & 255) == 0) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][(threadIdx.x >> 8) * kProfPhases + i_] = prof_acc[i_]; } while (0)
 // waves 0 and 3 (the split K1's preparer): [.][0..7] and [.][8..15]
 #define PROF_STORE_W03 do { if (threadIdx.x == 0 || threadIdx.x == 192) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][(threadIdx.x ? kProfPhases : 0) + i_] = prof_acc[i_]; } while (0)
+// waves 0 and 7 (the 32-channel split K1's preparer): [.][0..7] and [.][8..15]
+#define PROF_STORE_W07 do { if (threadIdx.x == 0 || threadIdx.x == 448) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][(threadIdx.x ? kProfPhases : 0) + i_] = prof_acc[i_]; } while (0)
 #else
+#define PROF_STORE_W07 do {} while (0)
 #define PROF_STORE_W03 do {} while (0)
 #define PROF_STORE_W04 do {} while (0)
 #define PROF_DECL

@@ -119,6 +119,11 @@ def run(reps=15, rounds=3):
                  "barrier_after_groups", "loop_top"]
         sets = [("wave 0 (SIMD 0, older)", names, full[:, :8]),
                 ("wave 3 (SIMD 3, preparer)", names, full[:, 8:])]
+    elif os.environ.get("ABLATE_PROF_SETS") == "w07":   # the 32-channel split K1: wave 0 and the preparer wave 7
+        names = ["preparer", "phase0_gather+perc", "phase1_staging", "phase1_gather+perc", "next_stage",
+                 "mfma+epi", "partials+barrier", "loop_top"]
+        sets = [("wave 0 (SIMD 0, group)", names, full[:, :8]),
+                ("wave 7 (preparer / stager)", names, full[:, 8:])]
     elif os.environ.get("ABLATE_PROF_SETS") == "w04":   # the split K1: both waves of SIMD 0
         names = ["dma_issue", "fire+dma_wait", "planes", "compaction", "groups", "reduction",
                  "top_barrier", "loop_tail"]
