@@ -200,8 +200,10 @@ template <int NT, bool GRAPH, bool TO_LDS>
 __device__ __forceinline__ void ks_fill_images(const K1Args& a, char* dst, int tid);
 
 #ifndef GNCA_K1_LEAN
-#define GNCA_K1_LEAN 2   // 2: the lean body as a software pipeline over the row blocks; 1: register-lean group body (one GEMM2 accumulator seeded with the message,
-                         // GEMM1 row blocks double-buffered through GEMM2); 0: round 2's body
+#define GNCA_K1_LEAN 1   // 1: register-lean group body (one GEMM2 accumulator seeded with the message, GEMM1 row
+                         // blocks double-buffered through GEMM2); 0: round 2's body; 2 (A/B builds): the lean body as
+                         // a row-block software pipeline -- 250 VGPRs leave no room for a co-resident K2 wave, so
+                         // the sub-batch pipeline's step is slower (0.540 vs 0.530 ms) although K1 alone is not
 #endif
 
 template <int NT, bool GRAPH, bool TO_LDS>
