@@ -899,7 +899,10 @@ __device__ __forceinline__ float k2_update(float x, float d, float sc, float sh,
 template <int V, bool COMPACT>
 __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_norm) {
   typedef float vf __attribute__((ext_vector_type(V)));
-  constexpr int KU = 2;   // main items per thread in flight (measured: 1: 0.184, 2: 0.178, 4: 0.187, 8: 0.207 ms)
+#ifndef GNCA_K2_KU
+#define GNCA_K2_KU 2
+#endif
+  constexpr int KU = GNCA_K2_KU;   // main items per thread in flight (measured alone: 1: 0.184, 2: 0.178, 4: 0.187, 8: 0.207 ms)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bj = blockIdx.x / a.nbands, band = blockIdx.x - bj * a.nbands;
   const int b = k2_sample(bj, a.B, a.zigzag);
@@ -1105,7 +1108,10 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
       // to V-1 floats past the live ones stays inside the workspace: the dx field is followed by
       // the GroupNorm partials)
       typedef float vfu __attribute__((ext_vector_type(V), aligned(4)));
-      constexpr int CU = 5;   // channels in flight per thread (B=1024 72^2: 3 0.164, 5 0.159, 8 0.183 ms)
+#ifndef GNCA_K2_CU
+#define GNCA_K2_CU 5
+#endif
+      constexpr int CU = GNCA_K2_CU;   // channels in flight per thread (alone, B=1024 72^2: 3 0.164, 5 0.159, 8 0.183 ms)
       for (int c0 = 0; c0 < C; c0 += CU) {
         vf xq[CU], fq[CU];
 #pragma unroll
