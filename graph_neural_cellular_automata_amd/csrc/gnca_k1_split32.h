@@ -28,14 +28,13 @@
 
 namespace gnca {
 
-#ifndef GNCA_S32_PREP_PRIO
-#define GNCA_S32_PREP_PRIO 3
+#ifndef GNCA_S32_PREP_SPLIT
+#define GNCA_S32_PREP_SPLIT 0   // A/B builds: the next tile's sender plane and its live list by two waves side by side
+                                // (c5 step 0.660 vs 0.656 ms with the preparer alone: not kept)
 #endif
 
-#ifndef GNCA_S32_LATE_PREP
-#define GNCA_S32_LATE_PREP 0   // the preparer builds the next tile's slot after the phase-1 staging (under
-                               // the groups' phase-1 reads and MFMAs) instead of beside phase 0, and
-                               // leaves the next tile's phase-0 DMA to the other waves without a group
+#ifndef GNCA_S32_PREP_PRIO
+#define GNCA_S32_PREP_PRIO 3
 #endif
 
 #ifndef GNCA_S32_STAGERS
@@ -155,7 +154,10 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   // The preparer (one wave): tile t's sender plane over the region, keep = fire AND pre-alive, the
   // live-cell list into slot s, the compact field's row tables (and, dense field, the dead cells'
   // zeros).  The pre-update masks are the alive bytes (the previous K2's, or gnca_k_alive's).
-  auto prep = [&](int t, int s) {
+  // part: 3 = everything (one wave), 1 = the region's sender plane only, 2 = the keep mask, live
+  // list and row tables only (keep bits from the alive bytes in global memory): with a second wave
+  // without a group the two halves run side by side
+  auto prep = [&](int t, int s, int part) {
     // the preparer (the younger wave of its SIMD, beside a group wave) at the top issue priority
     // while it prepares: it is on the tile's critical path (c5 K1 0.559 -> 0.534 ms)
     if (GNCA_S32_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_S32_PREP_PRIO);
@@ -167,11 +169,10 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     uint8_t* lstp = reinterpret_cast<uint8_t*>(smem_b + L.lst + s * L.lst_slot);
     uint8_t* abq = reinterpret_cast<uint8_t*>(smem_b + L.ab);
     uint64_t* cb = reinterpret_cast<uint64_t*>(smem_b + L.cb);
-    {
+    if (part & 1) {
       const uint8_t* alb = a.alive + (size_t)b * HW;
       constexpr int NU = (RHW + 63) / 64;
-      // (late prep: NB loads in flight per batch, few registers beside the held phase-0 fragments)
-      constexpr int NB = GNCA_S32_LATE_PREP ? 4 : NU;
+      constexpr int NB = NU;
 #pragma unroll 1
       for (int u0 = 0; u0 < NU; u0 += NB) {
         uint32_t v[NB];
@@ -200,16 +201,33 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!(part & 2)) {
+      if (GNCA_S32_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(0);
+      return;
+    }
+    // the tile cells' alive bytes: from the region plane this wave just built, or (list half alone)
+    // straight from global memory, every chunk's load in flight together
+    constexpr int NCH = (NCELL + 63) / 64;
+    uint32_t cab[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int n = 64 * ch + lane;
+      const int ti = n / TW, tj = n - (n / TW) * TW;
+      cab[ch] = 0u;
+      if (n < NCELL)
+        cab[ch] = (part & 1) ? abq[(ti + RY) * RW + tj + RX]
+                             : a.alive[(size_t)b * HW + (size_t)(i0 + ti) * W + (j0 + tj)];
+    }
     float* outb = a.out + (size_t)b * C * HW + cell0;
     int nl = 0;
-#pragma unroll 1
+#pragma unroll
     for (int n0 = 0; n0 < NCELL; n0 += 64) {
       const int n = n0 + lane;
       const bool inb = n < NCELL;
       const int ti = n / TW, tj = n - (n / TW) * TW;
       const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
       bool live = false;
-      if (inb && (abq[(ti + RY) * RW + tj + RX] & 1u))
+      if (inb && (cab[n0 >> 6] & 1u))
         live = fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step, a.sample_base, b, HW, cell);
       const uint64_t bal = __ballot(live);
       const int pre = __popcll(bal & ((1ull << lane) - 1ull));
@@ -244,7 +262,7 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
   // prologue: the first tile's phase-0 DMA and planes, then the weight images
   int tile = next_active(t_begin + xr_);
   if (tile < t_end) stage(tile, 0, wave, NW);
-  if (wave == PW && tile < t_end) prep(tile, 0);
+  if (wave == PW && tile < t_end) prep(tile, 0, 3);
   if (tid == 0) *xsd = 0;
 
   // ---- weight images (bf16 parts in MFMA fragment order), once per persistent workgroup ----
@@ -339,8 +357,13 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     const uint8_t* sp = reinterpret_cast<const uint8_t*>(smem_b + L.sp + par * L.sp_slot);
     const uint8_t* lst = reinterpret_cast<const uint8_t*>(smem_b + L.lst + par * L.lst_slot);
     const int nlive = cnt[par];
-    // (late prep: at the tile start only when the preparer has a group itself, > 224 live cells)
-    if (wave == PW && nxt < t_end && (!GNCA_S32_LATE_PREP || 32 * PW < nlive)) prep(nxt, par ^ 1);
+    // the next tile's slot: wave PW - 1 builds the sender plane beside the preparer's list when it
+    // has no group itself (<= 192 live cells), else the preparer does both
+    if (nxt < t_end) {
+      const bool two = GNCA_S32_PREP_SPLIT && 32 * (PW - 1) >= nlive;
+      if (wave == PW) prep(nxt, par ^ 1, two ? 2 : 3);
+      else if (two && wave == PW - 1) prep(nxt, par ^ 1, 1);
+    }
     PROF_MARK(0);   // preparer
 
     // ---- one 32-cell group per wave; its accumulators live across the two channel phases ----
@@ -366,10 +389,6 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         PROF_MARK(2);   // phase-1 staging (barrier, DMA, wait, barrier)
-        if (GNCA_S32_LATE_PREP && wave == PW && !has && nxt < t_end) {
-          prep(nxt, par ^ 1);
-          PROF_MARK(0);
-        }
       }
       if (!has) continue;
       // -- gather of alive-masked x, this phase's channels 16ph + 8h + j (uniform weight 1/k) --
@@ -481,10 +500,8 @@ __global__ __launch_bounds__(512, 1) void gnca_k1_split32(const K1Args a) {
     // alone when all 8 waves have one; the 208 LDS-DMA instructions of a phase issued by one wave
     // take longer than the groups' MFMAs (~60-100 cycles each beside MFMAs)
 #if GNCA_S32_STAGERS
-    // (late prep: the preparer stages only when it is the one wave without a group)
-    const int nidle = NW - ngrp - ((GNCA_S32_LATE_PREP && ngrp < NW - 1) ? 1 : 0);
-    const int nst = nidle > 0 ? nidle : 1;
-    const bool stager = nidle > 0 ? (wave >= ngrp && wave < ngrp + nidle) : wave == PW;
+    const int nst = ngrp < NW ? NW - ngrp : 1;
+    const bool stager = ngrp < NW ? wave >= ngrp : wave == PW;
 #else
     const int nst = 1;
     const bool stager = wave == PW;
