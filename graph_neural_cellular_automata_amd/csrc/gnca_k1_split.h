@@ -446,14 +446,29 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     // (2) keep = fire AND pre-alive per 64-cell chunk; live cells listed in cell order
     float* outb = a.out + (size_t)b * C * HW + cell0;
     int nl = 0;
-#pragma unroll 1
+    // small tiles (<= 4 chunks, the small-batch variants, where the first tile's prep is on the
+    // launch's critical path): every chunk's alive byte read at once and the loop unrolled
+    constexpr int NCH = (NCELL + 63) / 64;
+    constexpr bool SMALLT = NCH <= 4;
+    constexpr int CUNR = SMALLT ? 4 : 1;
+    uint32_t cab[SMALLT ? NCH : 1];
+    if constexpr (SMALLT) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int n = 64 * ch + lane;
+        const int ti = n / TW, tj = n - (n / TW) * TW;
+        cab[ch] = n < NCELL ? abq[(ti + RY) * RW + tj + RX] : 0u;
+      }
+    }
+#pragma unroll CUNR
     for (int n0 = 0; n0 < NCELL; n0 += 64) {
       const int n = n0 + lane;
       const bool inb = n < NCELL;
       const int ti = n / TW, tj = n - (n / TW) * TW;
       const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
       bool live = false;
-      if (inb && (abq[(ti + RY) * RW + tj + RX] & 1u))
+      const uint32_t ab_ = SMALLT ? cab[SMALLT ? (n0 >> 6) : 0] : (inb ? abq[(ti + RY) * RW + tj + RX] : 0u);
+      if (inb && (ab_ & 1u))
         live = (GNCA_ABLATE & kAblFire) ? ((cell & 1) != 0)
                                         : fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step,
                                                   a.sample_base, b, HW, cell);
@@ -494,7 +509,9 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   // that tile, then every weight load of this thread in flight together, then the weight images'
   // splits and LDS stores (B=8 72^2 K1: 20.0 -> 19.8 us; the preparer after the weight loads 22.3 us)
   if (tile < t_end) issue_dma(tile, wave, NW);
+  PROF_MARK(0);   // (prologue) first tile's DMA issue
   if (wave == PW && tile < t_end) prep(tile, 0);
+  PROF_MARK(3);   // (prologue) first tile's prep
   float pcv = 0.f;
   if (tid < C * 27) pcv = a.perc[tid];
   if (tid == 0) { *gctr = 0; *xsd = 0; }
@@ -516,7 +533,9 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     // the perception zero tap: every channel plane's pad floats (never written by the staging)
     for (int e = tid; e < 16 * (PSTR - RHW); e += NT) xs[(e / (PSTR - RHW)) * PSTR + RHW + e % (PSTR - RHW)] = 0.f;
   }
+  PROF_MARK(2);   // (prologue) weight image copy / fill issue
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PROF_MARK(1);   // (prologue) wait for the DMA, images and weight loads
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch; the
   // other case reads the weights from global memory, an uncommon slow path)
   int ok = 1;
