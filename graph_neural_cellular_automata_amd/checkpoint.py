@@ -29,11 +29,30 @@ def _epoch_num(name: str) -> int:
     return int(m.group(1)) if m else -1
 
 
+def pool_rng_states(pool) -> dict | None:
+    """Every rank's private slot-index stream of a sharded ``SamplePool``, as
+    ``{"world": W, "ranks": {rank: state}}``.  Collective when ``torch.distributed`` is initialised
+    with the pool's world (every rank must call it; then every rank gets the whole map); otherwise
+    only this process's rank is in the map.  None for an unsharded pool (it uses the global stream,
+    which is the caller's to save)."""
+    if pool is None or pool.rng_state() is None:
+        return None
+    import torch.distributed as dist
+    mine = pool.rng_state()
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() == pool.world > 1:
+        got = [None] * pool.world
+        dist.all_gather_object(got, (pool.rank, mine))
+        return {"world": pool.world, "ranks": {int(r): st for r, st in got}}
+    return {"world": pool.world, "ranks": {pool.rank: mine}}
+
+
 def save_checkpoint(ckpt_dir, tag, model, optimizer, scheduler, epoch, global_step, config=None,
-                    *, latest: bool = False, pool=None) -> str:
-    """Write ``<ckpt_dir>/nca_<tag>.pt`` (and ``nca_latest.pt`` when ``latest``).  ``pool``: a
-    sharded ``SamplePool`` whose private slot-index stream is saved too (``pool_rng_state``), so a
-    resumed run continues its sequence (an extra key; the reference trainer ignores it)."""
+                    *, latest: bool = False, pool=None, pool_states: dict | None = None) -> str:
+    """Write ``<ckpt_dir>/nca_<tag>.pt`` (and ``nca_latest.pt`` when ``latest``).  The private
+    slot-index streams of a sharded ``SamplePool`` are saved too (``pool_rng_state``, an extra key
+    the reference trainer ignores), per rank, so a resumed run continues EACH rank's sequence:
+    pass ``pool_states`` from ``pool_rng_states(pool)`` (called on every rank; then only rank 0
+    needs to save), or ``pool`` to store this process's rank only."""
     os.makedirs(ckpt_dir, exist_ok=True)
     payload = {
         "epoch": int(epoch),
@@ -44,8 +63,11 @@ def save_checkpoint(ckpt_dir, tag, model, optimizer, scheduler, epoch, global_st
         "param_count": count_parameters(model),
         "global_step": int(global_step),
     }
-    if pool is not None and pool.rng_state() is not None:
-        payload["pool_rng_state"] = pool.rng_state()
+    if pool_states is None and pool is not None:
+        pool_states = pool_rng_states(pool) if pool.world == 1 else \
+            {"world": pool.world, "ranks": {pool.rank: pool.rng_state()}}
+    if pool_states is not None:
+        payload["pool_rng_state"] = pool_states
     path = os.path.join(ckpt_dir, f"nca_{tag}.pt")
     torch.save(payload, path)
     if latest:
@@ -95,6 +117,19 @@ def load_checkpoint(payload, model, optimizer=None, scheduler=None, pool=None) -
             scheduler.load_state_dict(payload["scheduler_state"])
         except Exception as e:
             print(f"[warn] scheduler state not compatible, reinit: {e}", flush=True)
-    if pool is not None and payload.get("pool_rng_state") is not None:
-        pool.set_rng_state(payload["pool_rng_state"])
+    saved = payload.get("pool_rng_state")
+    if pool is not None and saved is not None and pool.rng_state() is not None:
+        if isinstance(saved, dict) and "ranks" in saved:
+            ranks = {int(r): st for r, st in saved["ranks"].items()}
+            if int(saved.get("world", -1)) != pool.world:
+                print(f"[warn] pool streams were saved for world {saved.get('world')}, this run has "
+                      f"world {pool.world}: the pool keeps its fresh stream", flush=True)
+            elif pool.rank not in ranks:
+                print(f"[warn] no saved pool stream for rank {pool.rank}: the pool keeps its fresh "
+                      f"stream", flush=True)
+            else:
+                pool.set_rng_state(ranks[pool.rank])
+        else:   # a single unlabelled stream (older checkpoints): whose rank it was is unknown
+            print("[warn] checkpoint holds one unlabelled pool stream: the pool keeps its fresh "
+                  "stream", flush=True)
     return int(payload.get("epoch", 0)) + 1

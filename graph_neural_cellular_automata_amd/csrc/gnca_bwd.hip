@@ -1686,6 +1686,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
                       const gnca_grads* grads, const void* saved, void* ws, size_t ws_bytes,
                       void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  StreamDeviceGuard dg(st);
   if (!desc || !w || !x || !gy || !gx || !grads) return GNCA_ERR_INVALID;
   if (gx == x || gx == gy) return GNCA_ERR_INVALID;
   gnca_step_desc d = *desc;

@@ -33,6 +33,26 @@ __device__ __forceinline__ void wg_stamp(uint64_t* st, int which) {
 }
 #define GNCA_STAMP_END(st) do { if ((st) != nullptr) { __syncthreads(); wg_stamp((st), 1); } } while (0)
 
+// Host: the device that owns `stream` is made current for the scope of an entry point and the
+// caller's current device restored on exit, so the per-device caches (CU count, occupancy,
+// helper streams and events) and every launch refer to the stream's device even when the caller
+// passes a stream of a device that is not current (e.g. a cuda:1 tensor while cuda:0 is current).
+struct StreamDeviceGuard {
+  int prev = -1;
+  explicit StreamDeviceGuard(hipStream_t stream) {
+    int cur = 0;
+    hipDevice_t dev = 0;
+    if (stream == nullptr || hipGetDevice(&cur) != hipSuccess) return;
+    if (hipStreamGetDevice(stream, &dev) != hipSuccess || (int)dev == cur) return;
+    if (hipSetDevice((int)dev) == hipSuccess) prev = cur;
+  }
+  ~StreamDeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  StreamDeviceGuard(const StreamDeviceGuard&) = delete;
+  StreamDeviceGuard& operator=(const StreamDeviceGuard&) = delete;
+};
+
 __device__ __forceinline__ int wrapi(int v, int n) {
   v %= n;
   return v < 0 ? v + n : v;

@@ -1945,12 +1945,14 @@ int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* 
 
 int gnca_step_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x, float* x_out,
                   const void* fire, float* attn, void* ws, size_t ws_bytes, void* stream) {
+  StreamDeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
   return step_impl(desc, w, x, x_out, fire, attn, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream));
 }
 
 int gnca_step_masked_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
                          float* x_out, const void* fire, const uint8_t* active, void* ws,
                          size_t ws_bytes, void* stream) {
+  StreamDeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
   if (!active || (desc && (desc->flags & GNCA_ATTENTION))) return GNCA_ERR_INVALID;
   return step_impl(desc, w, x, x_out, fire, nullptr, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream),
                    GNCA_PHASE_ALL, active);
@@ -1959,6 +1961,7 @@ int gnca_step_masked_f32(const gnca_step_desc* desc, const gnca_weights* w, cons
 int gnca_step_phases_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
                          float* x_out, const void* fire, float* attn, void* ws, size_t ws_bytes,
                          void* stream, uint32_t phases) {
+  StreamDeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
   const bool alive = (phases & GNCA_PHASE_ALIVE) && desc && desc->alpha_thr >= 0.f &&
                      desc->graph_alpha_thr >= desc->alpha_thr;
   return step_impl(desc, w, x, x_out, fire, attn, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream),
@@ -1967,6 +1970,7 @@ int gnca_step_phases_f32(const gnca_step_desc* desc, const gnca_weights* w, cons
 
 int gnca_message_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
                      float* message, float* attn, void* ws, size_t ws_bytes, void* stream) {
+  StreamDeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (!desc || !(desc->flags & GNCA_GRAPH)) return GNCA_ERR_INVALID;
   Plan P;
@@ -2003,6 +2007,7 @@ int gnca_message_f32(const gnca_step_desc* desc, const gnca_weights* w, const fl
 
 int gnca_perceive_f32(int32_t B, int32_t C, int32_t H, int32_t W, const float* weight,
                       const float* x, float* y, void* stream) {
+  StreamDeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || !weight || !x || !y) return GNCA_ERR_INVALID;
   const size_t total = (size_t)B * C * H * W;
   size_t blocks = (total + kThreads - 1) / kThreads;
@@ -2019,6 +2024,7 @@ int gnca_prof_dump(unsigned long long* out) {
 #endif
 
 int gnca_fire_mask_u8(const gnca_step_desc* desc, uint8_t* mask, void* stream) {
+  StreamDeviceGuard dg(reinterpret_cast<hipStream_t>(stream));
   if (!desc || !mask || desc->B <= 0 || desc->H <= 0 || desc->W <= 0) return GNCA_ERR_INVALID;
   const size_t total = (size_t)desc->B * desc->H * desc->W;
   size_t blocks = (total + kThreads - 1) / kThreads;
@@ -2039,9 +2045,13 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
   if (flags & ~(uint32_t)(GNCA_ROLLOUT_ALIVE_IN | GNCA_ROLLOUT_ALIVE_OUT)) return GNCA_ERR_INVALID;
   if (desc->fire_mode != GNCA_FIRE_NONE && desc->fire_mode != GNCA_FIRE_HASH) return GNCA_ERR_INVALID;
   if (x == x_final || x == scratch || x_final == scratch) return GNCA_ERR_INVALID;
+  // a zero-step piece of a rollout issued in pieces would have to order its copy after the other
+  // sub-batch streams' work (and join them if it is the last piece): not a meaningful call
+  if (steps == 0 && flags != 0) return GNCA_ERR_INVALID;
   const int k = desc->num_offsets;
   if ((desc->flags & GNCA_GRAPH) && k > 0 && !offsets) return GNCA_ERR_INVALID;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  StreamDeviceGuard dg(st);   // helper streams, events and CU counts of the stream's device
   if (steps == 0)
     return hipMemcpyAsync(x_final, x, (size_t)desc->B * desc->C * desc->H * desc->W * sizeof(float),
                           hipMemcpyDeviceToDevice, st) == hipSuccess ? GNCA_OK : GNCA_ERR_HIP;

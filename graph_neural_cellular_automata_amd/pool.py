@@ -34,6 +34,7 @@ class SamplePool:
         pool slot exactly as the reference does (pool.py:18)."""
         self.pool_size = int(pool_size)
         rank, world = shard if shard is not None else (0, 1)
+        self.rank, self.world = int(rank), int(world)
         self.lo, self.hi = shard_range(self.pool_size, rank, world)
         seeds = []
         for i in range(self.pool_size):

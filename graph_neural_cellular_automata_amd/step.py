@@ -76,23 +76,27 @@ def make_weights(tensors: dict) -> tuple[L.Weights, list]:
     contiguous tensors that must stay alive until the launch is enqueued.
 
     When every tensor is already a contiguous float32 device tensor the struct holds exactly their
-    addresses, so it is cached by (device, name, address): a hit rebuilds nothing (in-place updates
-    such as optimiser steps keep the addresses), and because the struct is a pure function of the
-    key the cache holds no tensor references (the weights of a deleted model are freed; a later
-    tensor at the same address gets the same, correct struct).  Building the struct was ~20 us of
-    host time per step at the trainer's size."""
-    key = tuple((name, t.device.index, t.data_ptr()) for name, t in tensors.items() if t is not None)
+    addresses, so it is cached by (name, device, address, shape): a hit rebuilds nothing (in-place
+    updates such as optimiser steps keep the addresses).  Only such tensors are looked up or
+    stored: the check runs BEFORE the lookup, so a non-contiguous view or a tensor of another dtype
+    that happens to sit at a cached address never returns a cached struct.  For cacheable tensors
+    the struct is a pure function of the key, so the cache holds no tensor references (the weights
+    of a deleted model are freed; a later tensor at the same address gets the same, correct
+    struct).  Building the struct was ~20 us of host time per step at the trainer's size."""
     keep = [t for t in tensors.values() if t is not None]
-    hit = _WCACHE.get(key)
-    if hit is not None:
-        return hit, keep
+    cacheable = all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() for t in keep)
+    key = None
+    if cacheable:
+        key = tuple((name, t.device.index, t.data_ptr(), tuple(t.shape))
+                    for name, t in tensors.items() if t is not None)
+        hit = _WCACHE.get(key)
+        if hit is not None:
+            return hit, keep
     w = L.Weights()
-    cacheable = True
     conv = []
     for name, t in tensors.items():
         if t is None:
             continue
-        cacheable &= t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
         t = _dev_f32(t.detach(), name)
         conv.append(t)
         setattr(w, name, t.data_ptr())
@@ -152,6 +156,16 @@ def rollout_subs(desc: L.StepDesc) -> int:
     arith = ctypes.c_int32(0)
     L.check(L.load().gnca_k1_variant(ctypes.byref(desc), buf, 128, ctypes.byref(arith)), "gnca_k1_variant")
     return 2 if arith.value & 4 else 1
+
+
+def rollout_fold(desc: L.StepDesc) -> bool:
+    """True when a rollout of ``desc``'s shape folds each step's finalize (GroupNorm, tanh * gain,
+    residual, post-update alpha gate) into the next step's K1, so one K1 launch per step plus one
+    K2 at the end of the rollout (gnca_k1_variant arith bit 8)."""
+    buf = ctypes.create_string_buffer(128)
+    arith = ctypes.c_int32(0)
+    L.check(L.load().gnca_k1_variant(ctypes.byref(desc), buf, 128, ctypes.byref(arith)), "gnca_k1_variant")
+    return bool(arith.value & 8)
 
 
 def stream_ptr(device) -> int:

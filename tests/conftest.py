@@ -8,5 +8,23 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+# The multi-rank GPU tests (test_gpu_multirank.py) start their ranks as forks of a forkserver that
+# is started HERE, before any test touches the GPU: on the GPU pool a process that has initialised
+# the GPU must never exec another program, and a forkserver child never execs at all.
+FORKSERVER_READY = False
+
+
 def pytest_configure(config):
+    global FORKSERVER_READY
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); runs through the C-ABI")
+    if "not gpu" in (config.getoption("markexpr") or ""):
+        return
+    import multiprocessing as mp
+    import multiprocessing.forkserver as fs
+
+    import torch
+    if torch.cuda.device_count() == 0:   # counts devices without initialising HIP
+        return
+    mp.get_context("forkserver").set_forkserver_preload([])
+    fs.ensure_running()
+    FORKSERVER_READY = True

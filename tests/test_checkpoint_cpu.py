@@ -55,3 +55,41 @@ def test_round_trip_and_resume_choice(tmp_path):
 
 def test_empty_dir_has_no_resume(tmp_path):
     assert pick_resume(tmp_path) == (None, None)
+
+
+def test_sharded_pool_streams_resume_per_rank(tmp_path):
+    """Each rank's private pool stream is saved under its rank and restored into the pool of the
+    same rank (pool.py's per-rank streams), so a resumed 2-rank run continues both sequences; a
+    checkpoint from another world size leaves the streams as they are."""
+    import random
+
+    from graph_neural_cellular_automata_amd.checkpoint import pool_rng_states
+    from graph_neural_cellular_automata_amd.pool import SamplePool
+
+    def seed_fn(batch_size=1):
+        return torch.zeros(batch_size, 4, 2, 2)
+
+    def pools(world):
+        random.seed(5)
+        return [SamplePool(16, seed_fn, shard=(r, world)) for r in range(world)]
+
+    live = pools(2)
+    for p in live:
+        p.sample(3)
+    states = {"world": 2, "ranks": {}}
+    for p in live:                     # what pool_rng_states gathers over a process group
+        states["ranks"].update(pool_rng_states(p)["ranks"])
+    m = _model()
+    opt, sch = _opt(m)
+    path = save_checkpoint(tmp_path, "epoch1", m, opt, sch, epoch=1, global_step=2, pool_states=states)
+    payload = torch.load(path, map_location="cpu", weights_only=True)
+    expect = [p.sample(3)[0] for p in live]
+    fresh = pools(2)
+    for p in fresh:
+        load_checkpoint(payload, _model(), pool=p)
+    assert [p.sample(3)[0] for p in fresh] == expect
+    assert expect[0] != expect[1]      # the ranks' streams differ
+    other = pools(4)[1]
+    before = other.rng_state()
+    load_checkpoint(payload, _model(), pool=other)
+    assert other.rng_state() == before

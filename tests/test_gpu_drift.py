@@ -8,7 +8,10 @@ with the oracle stepped in float64 on the same offsets and hashed fire masks (gl
 ``sample_base + i``).  Reference path: ``ncagraph.py:106-168`` (graph), ``nca.py:64-105`` (classic).
 Weights: the reference's trained checkpoints carried by the golden fixtures (graph nca_latest.pt,
 classic nca_epoch980.pt) or, for 32 channels, the fixture's seeded init (W2 ~ N(0, 0.02))."""
+import json
+import os
 import random
+import time
 
 import numpy as np
 import pytest
@@ -19,18 +22,29 @@ from tests.golden_io import Case
 
 pytestmark = pytest.mark.gpu
 
-# case -> (fixture, graph, C, H, B, R, K, steps, samples checked, expected K1)
+# case -> (fixture, graph, C, H, B, R, K, steps, samples checked, expected K1, compact field)
 CASES = {
     # the headline's shape class: B=96 x 16 x 72^2 graph torus r=4 K=8 -> 576 tiles of 24x36
     "graph_split24x36": ("graph_torus_latest_grown_b1_72", True, 16, 72, 96, 4, 8, 96, (0, 47, 95),
-                         "gnca_k1_split<24,36,4,4,8>"),
+                         "gnca_k1_split<24,36,4,4,8>", True),
     # classic NCA (BASELINE config 2's step) on the classic split K1
     "classic_split8x24": ("classic_ep980_b2_32", False, 16, 72, 96, 0, 0, 96, (0, 47, 95),
-                          "gnca_k1_split<8,24,1,4,0>"),
-    # BASELINE config 5's shape class: 32 ch, 128^2, r=5, K=16 (48 steps: the f64 oracle's time)
-    "c5_split32": ("graph_torus_c32_r5_k16_b1_48", True, 32, 128, 8, 5, 16, 48, (0, 7),
-                   "gnca_k1_split32<16,16,5,8,16>"),
+                          "gnca_k1_split<8,24,1,4,0>", True),
+    # BASELINE config 3 (graph torus r=4 K=8, B=8, 72^2): the small-batch split K1 on 8x24 tiles,
+    # dense update field
+    "c3_split8x24": ("graph_torus_latest_grown_b1_72", True, 16, 72, 8, 4, 8, 96, (0, 7),
+                     "gnca_k1_split<8,24,4,4,8>", False),
+    # the graph trainer's rollout shape (B=16, 40^2, config.json): 8x20 tiles, dense update field
+    "trainer_split8x20": ("graph_torus_latest_grown_b1_72", True, 16, 40, 16, 4, 8, 96, (0, 15),
+                          "gnca_k1_split<8,20,4,4,8>", False),
+    # BASELINE config 5's shape class: 32 ch, 128^2, r=5, K=16 (48 steps: the f64 oracle's time);
+    # B=16 gives 1024 tiles, above the compact field's 2-per-CU threshold on 256- and 304-CU parts
+    "c5_split32": ("graph_torus_c32_r5_k16_b1_48", True, 32, 128, 16, 5, 16, 48, (0, 15),
+                   "gnca_k1_split32<16,16,5,8,16>", True),
 }
+# every case's max |hip - f64| is appended here (JSON lines; the GPU box merges gpurun_out/ back)
+DRIFT_LOG = os.environ.get("GNCA_DRIFT_LOG", os.path.join(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__))), "gpurun_out", "drift_log.jsonl"))
 GAIN, THR, MSG, FIRE, SEED = 0.05, 0.12, 0.25, 0.5, 5
 
 
@@ -45,7 +59,7 @@ def dev():
 def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
-    fx, graph, C, H, B, R, K, T, check, k1_expected = CASES[case]
+    fx, graph, C, H, B, R, K, T, check, k1_expected, compact = CASES[case]
     c = Case(fx)
     p64 = {k: v.astype(np.float64) for k, v in c.weights.items()}
     wt = {k: torch.from_numpy(np.ascontiguousarray(v.astype(np.float32))).to(dev) for k, v in c.weights.items()}
@@ -72,7 +86,7 @@ def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
                     fire_mode=L.FIRE_HASH, rng_seed=SEED, rng_step=0, sample_base=base)
     name, arith = S.k1_variant(d)
     assert (name, arith) == (k1_expected, "bf16x6")
-    assert S.rollout_compact(d), "the rollout must run on the compact update field"
+    assert S.rollout_compact(d) == compact, "the rollout's update-field layout"
     got = S.rollout(d, w, x.contiguous(), T, offs).cpu().numpy()
     assert np.isfinite(got).all()
     cfg = dict(update_gain=GAIN, alpha_thr=THR, use_groupnorm=True, graph=graph, message_gain=MSG,
@@ -82,7 +96,14 @@ def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
     for t in range(T):
         fm = np.concatenate([O.hash_fire_mask(SEED, t, base + int(i), 1, H, H, FIRE) for i in idx])
         ref = O.nca_step(ref, p64, cfg, chosen=offs[t] if graph else None, fire_mask=fm)
-    err = np.abs(got[idx] - ref).max()
+    err = float(np.abs(got[idx] - ref).max())
+    flips = int((O.alive_mask(got[idx], THR) != O.alive_mask(ref, THR)).sum())
     print(f"[drift] {case}: {name}, {T} steps, samples {list(check)}: max |hip - f64| = {err:.3e}")
+    os.makedirs(os.path.dirname(DRIFT_LOG), exist_ok=True)
+    with open(DRIFT_LOG, "a") as f:
+        f.write(json.dumps({"case": case, "k1": name, "compact": compact, "fold": S.rollout_fold(d),
+                            "batch": B, "canvas": H, "steps": T, "samples": list(check),
+                            "max_abs_err_vs_f64": err, "mean_abs_err_vs_f64": float(np.abs(got[idx] - ref).mean()),
+                            "alive_flips": flips, "tolerance": 1e-4, "time": time.time()}) + "\n")
     assert err <= 1e-4, err
     np.testing.assert_array_equal(O.alive_mask(got[idx], THR), O.alive_mask(ref, THR))

@@ -468,3 +468,19 @@ def test_subbatch_rollout_and_pieces_bitwise(dev):
                                         dst.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(), fl, st),
                 "gnca_rollout_ex_f32")
     assert torch.equal(b2, r)
+
+
+def test_make_weights_cache_rejects_non_contiguous_at_cached_address(dev):
+    """make_weights caches the struct of contiguous fp32 tensors by address; a non-contiguous view
+    (or another dtype) at a cached address must not hit the cache: it gets a contiguous copy."""
+    from graph_neural_cellular_automata_amd import step as S
+    t = torch.randn(16, 16, device=dev)
+    w_a, _ = S.make_weights({"w2": t})
+    assert w_a.w2 == t.data_ptr()
+    v = t.t()                                   # same address, transposed strides
+    assert v.data_ptr() == t.data_ptr() and not v.is_contiguous()
+    w_b, keep = S.make_weights({"w2": v})
+    assert w_b.w2 != t.data_ptr()
+    assert any(k.data_ptr() == w_b.w2 and torch.equal(k, v) for k in keep)
+    with pytest.raises(TypeError):
+        S.make_weights({"w2": t.view(torch.int32)})

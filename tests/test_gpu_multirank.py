@@ -1,0 +1,102 @@
+"""The multi-rank HIP path, test-backed (BASELINE config 4: the pool batch-sharded over GPUs, the
+gradient all-reduced before the trainer's normalisation, train_graph_augmented_nca.py:364-375).
+
+Two ranks share the box's one GPU over gloo (fresh forkserver children, tests/mr_workers.py):
+  * the sharded rollout (128 samples per rank, C4's per-GPU shard): the all-gathered states equal a
+    single-process HIP rollout of the same 256 samples BIT FOR BIT (fire hashed by global sample
+    index, per-sample GroupNorm: sharding.py);
+  * the data-parallel training step: each rank back-propagates the batch-mean loss of its half of
+    the batch through the HIP step, ``dp.allreduce_gradients`` averages the flat bucket, then the
+    trainer's policy; the result equals the single-process full-batch gradient after the same
+    policy within 1e-6 (``normalize``: the graph trainer's grad/||grad||; ``clip``: the classic
+    trainer's clip_grad_norm_, at a max norm the gradient exceeds).
+Plus a single-process check that a C4 shard (B=128) rolls out bitwise like the same samples of a
+B=1024 rollout."""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    return torch.device("cuda:0")
+
+
+def _run_ranks(target, args_of_rank, timeout=300):
+    import multiprocessing as mp
+
+    from tests import conftest
+    assert conftest.FORKSERVER_READY, "the forkserver must start before the GPU is initialised (conftest)"
+    ctx = mp.get_context("forkserver")
+    q = ctx.Queue()
+    port = 29900 + (os.getpid() % 500)
+    procs = [ctx.Process(target=target, args=(r, 2, port, *args_of_rank(q))) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = q.get(timeout=timeout)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert "error" not in res, res["error"]
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return res
+
+
+def test_two_rank_sharded_rollout_bitwise_equals_one_rank(dev, tmp_path):
+    from tests import mr_workers as M
+    out = str(tmp_path / "gathered.pt")
+    res = _run_ranks(M.rollout_rank, lambda q: (out, q))
+    assert res["world"] == 2
+    gathered = torch.load(out, weights_only=True)
+    spec = M.ROLL
+    ref, plan = M.hip_rollout(spec, M.roll_state(spec), 0, dev)
+    print(f"[multirank] rollout plans: ranks {res['plans']}, one rank {plan}")
+    assert res["plans"][0][0] == "gnca_k1_split<24,36,4,4,8>" and res["plans"][0][1], res["plans"]
+    assert torch.equal(gathered, ref.cpu())
+
+
+@pytest.mark.parametrize("policy", ["normalize", "clip"])
+def test_two_rank_dp_gradients_equal_full_batch(dev, policy):
+    from tests import mr_workers as M
+    spec = M.TRAIN
+    x, target = M.train_batch(spec)
+    # the full-batch gradient in this process (no all-reduce), and its norm for the clip's bound
+    avg_ref, _ = M.train_grads(spec, x, target, dev, "normalize", 0.0, False)
+    total = float(np.sqrt(sum((g ** 2).sum() for g in avg_ref.values())))
+    max_norm = 0.25 * total            # the clip must act: the case's norm exceeds its bound
+    _, post_ref = M.train_grads(spec, x, target, dev, policy, max_norm, False)
+    res = _run_ranks(M.train_rank, lambda q: (q, policy, max_norm))
+    assert sorted(res["avg"]) == sorted(avg_ref)
+    scale = 1.0 / max_norm if policy == "clip" else 1.0   # compare the clipped grads at unit norm
+    worst = 0.0
+    for k in avg_ref:
+        a, r = res["avg"][k], avg_ref[k]
+        assert np.abs(a - r).max() <= 1e-6 * max(np.abs(r).max(), 1e-30) + 1e-12, k
+        d = np.abs(res["post"][k] - post_ref[k]).max() * scale
+        worst = max(worst, d)
+        assert d <= 1e-6, (k, d)
+    print(f"[multirank] dp {policy}: |grad norm| {total:.3e}, max |2-rank - full batch| after the "
+          f"policy (unit scale) {worst:.2e}")
+
+
+def test_c4_shard_bitwise_equals_full_pool_rollout(dev):
+    """BASELINE config 4 on one GPU of eight: a 128-sample shard (sample_base 384) rolls out bitwise
+    like the same samples of the whole 1024-sample pool (different plans: the pool runs as two
+    sub-batches on two streams, the shard on one)."""
+    from tests import mr_workers as M
+    spec = dict(M.ROLL, B=1024, steps=6)
+    x = M.roll_state(spec)
+    full, plan_full = M.hip_rollout(spec, x, 0, dev)
+    shard, plan_shard = M.hip_rollout(spec, x[384:512], 384, dev)
+    print(f"[multirank] plans: pool {plan_full}, shard {plan_shard}")
+    assert torch.equal(full[384:512], shard)
