@@ -29,7 +29,7 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _run_ranks(target, args_of_rank, timeout=300):
+def _run_ranks(target, args_of_rank, timeout=100):
     import multiprocessing as mp
 
     from tests import conftest
