@@ -157,7 +157,7 @@ __host__ __device__ constexpr int ks_pstr(int rhw) {
 }
 
 struct KSLayout {
-  int xs, sp, ab, lst, cnt, cb, pg, w1, bias, w2, wm, wz, bml, total;   // byte offsets
+  int xs, sp, ab, lst, cnt, cb, pg, fk, p0, p1, pbm, w1, bias, w2, wm, wz, bml, total;   // byte offsets
   int sp_slot, lst_slot;                                             // bytes per prepared-tile slot
 };
 
@@ -177,9 +177,17 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   L.sp = o; o += 2 * L.sp_slot;           // sender plane (bytes 0/1), two slots
   L.ab = o; o += ks_a16(RHW);             // the preparer's alive bytes over the region
   L.lst = o; o += 2 * L.lst_slot;         // live-cell list (u16 cell indices), two slots
-  L.cnt = o; o += 16;                     // live cells per slot; group counter; staging-reads-done counter
+  L.cnt = o; o += 32;                     // live cells per slot; group counter; staging-reads-done counter;
+                                          // fold: finalize-item counter, preparations done
   L.cb = o; o += ks_a16(8 * (TH * TW / 64 + 2));   // the preparer's 64-cell chunk ballots
   L.pg = o; o += 2 * 16 * ((TH * TW + 31) / 32);  // per-group GroupNorm partials (fp64 pairs), two slots
+  // fold (gnca_k1_split<..., FOLD>): per slot the previous step's GroupNorm constants (48 floats) and
+  // the region's pre-update alive row masks P0 (one u64 per region row); the preparer's sender row
+  // masks P1 and its threshold-bit row masks of the pooled band (2 x (RH + 2) u64)
+  L.fk = o; o += 2 * 192;
+  L.p0 = o; o += 2 * ks_a16(RH * 8);
+  L.p1 = o; o += ks_a16(RH * 8);
+  L.pbm = o; o += ks_a16(2 * (RH + 2) * 8);
   L.w1 = o; o += 3 * 4 * 3 * 1024;       // [plane][rb][kc][lane] x 16 B
   L.bias = o; o += 4 * 32 * 16;          // [rb][row] x 16 B (k slots 0..2 = the three parts)
   L.w2 = o; o += 3 * 8 * 2 * 16 * 16;    // [plane][s][h][channel] x 16 B
@@ -316,7 +324,7 @@ __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst)
 #define GNCA_DMA_WAVES 1   // A/B builds: waves (the first failing pulls) sharing the next tile's DMA (3: K1 0.4015-0.4044 vs 0.4008-0.4026 ms with 1)
 #endif
 
-template <int TH, int TW, int RY, int RX, int KU>
+template <int TH, int TW, int RY, int RX, int KU, bool FOLD = false>
 __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_b[];
   constexpr int C = 16, HD = 128, NT = GNCA_K1_SPLIT_NT, NW = NT / 64;
@@ -345,9 +353,20 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   int* xsd = cnt + 3;
   int gbase = 0, xbase = 0;
   constexpr int NG = (TH * TW + 31) / 32;
+  // fold: finalize items (64 region quads x 4 channels) handed out by fctr; pdone counts the
+  // preparer's finished tiles (both monotonic over the workgroup's tiles, as gctr / xsd)
+  int* fctr = cnt + 4;
+  int* pdone = cnt + 5;
+  int fbase = 0;
+  constexpr int NQB = (NQ + 63) / 64, NFIN = 4 * NQB;
+  static_assert(!FOLD || (KU > 0 && C == 16), "the fold variant is the 16-channel graph K1");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   wg_stamp(a.stamps, 0);
+  if constexpr (FOLD) {   // the fold's counters are used before the prologue's barrier
+    if (tid == 0) { *fctr = 0; *pdone = 0; }
+    __syncthreads();
+  }
   if (GNCA_K1_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO);
   const int h = lane >> 5, r32 = lane & 31, c16 = lane & 15;
   const int H = a.H, W = a.W;
@@ -399,6 +418,205 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     }
   };
 
+  // ---- the fold (FOLD): the previous step's finalize, done here instead of by a K2 pass ----
+  // The preparer's part for a tile of sample b at (i0, j0), slot s: (F0) the previous step's per-
+  // sample GroupNorm constants (K2's fixed-order sums and arithmetic: fin_*); (F1) the finalized
+  // alpha x~_3 of the region plus one ring, as two threshold-bit row masks per row (ballots; lane =
+  // column of a band RW + 8 wide, quad-aligned); (F2) the 3x3 OR-pool of the bits with the
+  // max-pool's -inf border (no neighbour across the image edge, ncagraph.py:85-92) = the region's
+  // pre-update alive masks P0 (> alpha_thr) and sender masks P1 (> graph_alpha_thr), exactly the
+  // bytes K2 would have handed over; (F3) the sender plane from P1.
+  auto prep_fold = [&](int b, int i0, int j0, int s) {
+    float* fks = reinterpret_cast<float*>(smem_b + L.fk + s * 192);
+    uint64_t* p0s = reinterpret_cast<uint64_t*>(smem_b + L.p0 + s * ks_a16(RH * 8));
+    uint64_t* p1s = reinterpret_cast<uint64_t*>(smem_b + L.p1);
+    uint64_t* pbm = reinterpret_cast<uint64_t*>(smem_b + L.pbm);
+    uint32_t* spp = reinterpret_cast<uint32_t*>(smem_b + L.sp + s * L.sp_slot);
+    const bool gn = a.use_gn != 0;
+    float mu = 0.f, rs = 1.f;
+    if (gn) {
+      double t1, t2;
+      wave_sum2(a.statsp + (size_t)b * a.nst * 2, a.nst, &t1, &t2);
+      fin_mu_rs(t1, t2, (double)C * (double)HW, a.eps, &mu, &rs);
+    }
+    const float g3 = gn ? a.gamma[3] : 1.f, b3 = gn ? a.beta[3] : 0.f;
+    if (lane < C) {
+      float sc, sh;
+      fin_consts(gn ? a.gamma[lane] : 1.f, gn ? a.beta[lane] : 0.f, mu, rs, gn, &sc, &sh);
+      fks[lane] = sc;
+      fks[16 + lane] = sh;
+    }
+    if (lane == 0) {
+      fks[32] = mu;
+      fks[33] = rs;
+      fks[34] = g3;
+      fks[35] = b3;
+    }
+    constexpr int PBH = RH + 2, PBW = RW + 8, RB = (PBH + 1) / 2;
+    static_assert(PBW <= 64, "one lane per column of the pooled band");
+    const bool lin = lane < PBW;
+    int gcol = j0 - RX - 4 + (lin ? lane : 0);
+    gcol = gcol < 0 ? gcol + W : (gcol >= W ? gcol - W : gcol);
+    const int txS = gcol / TW, tjS = gcol - txS * TW;
+    const float* xpa = a.xp + ((size_t)b * C + 3) * HW;
+    const float* dpa = a.dxap + (size_t)b * HW;
+    const uint64_t* rmb = a.rmaskp + (size_t)b * a.tps * TH;
+#pragma unroll 1
+    for (int r0 = 0; r0 < PBH; r0 += RB) {
+      float xv[RB], dv[RB];
+      uint64_t mv[RB];
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        const int r = r0 + u;
+        int g = i0 - RY - 1 + r;
+        g = g < 0 ? g + H : (g >= H ? g - H : g);
+        const int tyS = g / TH, tiS = g - tyS * TH;
+        xv[u] = 0.f;
+        dv[u] = 0.f;
+        mv[u] = 0ull;
+        if (lin && r < PBH) {
+          const size_t cell = (size_t)g * W + gcol;
+          xv[u] = xpa[cell];
+          dv[u] = dpa[cell];
+          mv[u] = rmb[(size_t)(tyS * a.tiles_x + txS) * TH + tiS];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        const int r = r0 + u;
+        if (r < PBH) {
+          const bool live = ((mv[u] >> tjS) & 1ull) != 0;
+          const float xa = fin_alpha(xv[u], live ? dv[u] : 0.f, mu, rs, g3, b3, a.gain, gn);
+          const uint64_t b0 = __ballot(lin && xa > a.alpha_thr), b1 = __ballot(lin && xa > a.graph_alpha_thr);
+          if (lane == 0) {
+            pbm[r] = b0;
+            pbm[PBH + r] = b1;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // bit j of nf / nl: band column j is not the image's first / last column (its left / right
+    // neighbour in the band is its image neighbour, not the torus wrap)
+    const uint64_t nf = __ballot(lin && gcol != 0), nl = __ballot(lin && gcol != W - 1);
+    auto hz = [&](uint64_t m) { return m | ((m << 1) & nf) | ((m >> 1) & nl); };
+    if (lane < RH) {
+      int g = i0 - RY + lane;
+      g = g < 0 ? g + H : (g >= H ? g - H : g);
+      uint64_t q0 = hz(pbm[lane + 1]), q1 = hz(pbm[PBH + lane + 1]);
+      if (g > 0) {
+        q0 |= hz(pbm[lane]);
+        q1 |= hz(pbm[PBH + lane]);
+      }
+      if (g < H - 1) {
+        q0 |= hz(pbm[lane + 2]);
+        q1 |= hz(pbm[PBH + lane + 2]);
+      }
+      p0s[lane] = q0;
+      p1s[lane] = q1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if constexpr (GRAPH) {
+#pragma unroll 1
+      for (int e = lane; e < NQA; e += 64) {   // 4 sender bytes per dword (band column = region column + 4)
+        const int vr = e / QW, vc = 4 * (e - (e / QW) * QW);
+        const uint32_t bits = (uint32_t)(p1s[vr] >> (vc + 4)) & 15u;
+        spp[e] = a2a ? ((bits & 1u) | ((bits & 2u) << 7) | ((bits & 4u) << 14) | ((bits & 8u) << 21)) : 0x01010101u;
+      }
+    }
+  };
+
+  // The finalize of tile t's staged region (slot s: its constants and P0), into the staging buffer
+  // and, for the tile's own cells, into xo: x = x_prev + tanh(GN(dx_prev)) * gain (alpha: the
+  // updated alpha times the post-update gate P0), K2's arithmetic value for value.  Items of 64
+  // region quads x 4 channels are pulled from fctr by every wave that gets here; an item's loads
+  // (row tables, x_prev quads, the live cells' packed dx) are issued before the wait for the staging
+  // buffer to be free (every group of the current tile past its staged reads), so they overlap the
+  // other waves' last groups.
+  auto finalize = [&](int t, int s, int need_prep, bool wait_xsd, int qe, int xb) {
+    const int b = t / a.tps, tin = t - b * a.tps;
+    const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+    const int i0 = ty * TH, j0 = tx * TW;
+    while (__hip_atomic_load(pdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need_prep)
+      __builtin_amdgcn_s_sleep(1);
+    const float* fks = reinterpret_cast<const float*>(smem_b + L.fk + s * 192);
+    const uint64_t* p0s = reinterpret_cast<const uint64_t*>(smem_b + L.p0 + s * ks_a16(RH * 8));
+    const float mu = fks[32], rs = fks[33], g3 = fks[34], b3 = fks[35];
+    const bool gn = a.use_gn != 0;
+    const float g2 = -2.f * a.gain;
+    bool waited = !wait_xsd;
+#pragma unroll 1
+    for (;;) {
+      const int it = (__builtin_amdgcn_readfirstlane(atomicAdd(fctr, 1)) >> 6) - fbase;
+      if (it >= NFIN) break;
+      const int blk = it >> 2, cg = it & 3;
+      const int q = 64 * blk + lane;
+      const bool qv = q < NQ;
+      const int vr = qv ? q / QW : 0, vq = qv ? q - (q / QW) * QW : 0;
+      int g = i0 - RY + vr, gc = j0 - RX + 4 * vq;
+      g = g < 0 ? g + H : (g >= H ? g - H : g);
+      gc = gc < 0 ? gc + W : (gc >= W ? gc - W : gc);
+      const int tyS = g / TH, tiS = g - tyS * TH, txS = gc / TW, tjS = gc - txS * TW;
+      const uint32_t tsrc = (uint32_t)(b * a.tps + tyS * a.tiles_x + txS);
+      const uint64_t m = a.rmaskp[(size_t)tsrc * TH + tiS];
+      const uint32_t pre = a.rprep[(size_t)tsrc * TH + tiS];
+      const size_t cell = (size_t)g * W + gc;
+      f4 xq[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        xq[u] = *reinterpret_cast<const f4*>(a.xp + ((size_t)b * C + 4 * cg + u) * HW + cell);
+      f4 dqa = {0.f, 0.f, 0.f, 0.f};
+      if (cg == 0) dqa = *reinterpret_cast<const f4*>(a.dxap + (size_t)b * HW + cell);
+      // the quad's live cells are consecutive in the source tile's packed field: cell k's value (or,
+      // for a dead cell, the next live one's; never used) at rank r0 + (live cells before k)
+      const uint32_t bits = (uint32_t)(m >> tjS) & 15u;
+      const uint32_t r0 = tsrc * (uint32_t)(C * NCELL) + pre + (uint32_t)__popcll(m & ((1ull << tjS) - 1ull));
+      uint32_t off[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) off[k] = r0 + (uint32_t)__popc(bits & ((1u << k) - 1u));
+      float dv[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = 4 * cg + u;
+        const float* fb = a.dxp + (size_t)c * NCELL;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dv[u][k] = c == 3 ? 0.f : fb[off[k]];
+      }
+      if (!waited) {
+        while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xb < qe)
+          __builtin_amdgcn_s_sleep(1);
+        waited = true;
+      }
+      const bool own = vr >= RY && vr < RY + TH && vq >= RX / 4 && vq < (RX + TW) / 4;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = 4 * cg + u;
+        f4 v;
+        if (c == 3) {
+          const uint64_t pm = p0s[vr] >> (4 * vq + 4);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float xa = fin_alpha(xq[u][k], ((bits >> k) & 1u) ? dqa[k] : 0.f, mu, rs, g3, b3, a.gain, gn);
+            v[k] = xa * (((pm >> k) & 1ull) ? 1.f : 0.f);
+          }
+        } else {
+          const float sc = fks[c], sh = fks[16 + c];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = k2_update(xq[u][k], ((bits >> k) & 1u) ? dv[u][k] : 0.f, sc, sh, a.gain, g2);
+        }
+        if (qv) {
+          *reinterpret_cast<f4*>(xs + c * PSTR + 4 * q) = v;
+          if (own) *reinterpret_cast<f4*>(a.xo + ((size_t)b * C + c) * HW + cell) = v;
+        }
+      }
+    }
+    fbase += NFIN + NW;
+  };
+
   // The preparer (one wave, no workgroup barrier): a tile's sender plane over the region, its keep
   // mask (fire AND pre-alive) and live-cell list into slot `s`; the compact field's row tables and
   // the dead cells' zeros go to global memory.  The pre-update masks are the alive bytes (K2's
@@ -414,8 +632,12 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     uint32_t* abw = reinterpret_cast<uint32_t*>(smem_b + L.ab);
     const uint8_t* abq = reinterpret_cast<const uint8_t*>(smem_b + L.ab);
     uint64_t* cb = reinterpret_cast<uint64_t*>(smem_b + L.cb);
-    // (1) the region's alive bytes, 4 columns per dword, all loads in flight together
-    {
+    // (1) the region's alive bytes, 4 columns per dword, all loads in flight together (fold: the
+    //     masks from the finalized alpha, prep_fold)
+    const uint64_t* p0q = reinterpret_cast<const uint64_t*>(smem_b + L.p0 + s * ks_a16(RH * 8));
+    if constexpr (FOLD) {
+      prep_fold(b, i0, j0, s);
+    } else {
       const uint8_t* alb = a.alive + (size_t)b * HW;
       constexpr int NU = (NQA + 63) / 64;
       uint32_t v[NU];
@@ -467,7 +689,8 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       const int ti = n / TW, tj = n - (n / TW) * TW;
       const size_t cell = (size_t)(i0 + ti) * W + (j0 + tj);
       bool live = false;
-      const uint32_t ab_ = SMALLT ? cab[SMALLT ? (n0 >> 6) : 0] : (inb ? abq[(ti + RY) * RW + tj + RX] : 0u);
+      const uint32_t ab_ = FOLD ? (inb ? (uint32_t)(p0q[ti + RY] >> (tj + RX + 4)) & 1u : 0u)
+                                : SMALLT ? cab[SMALLT ? (n0 >> 6) : 0] : (inb ? abq[(ti + RY) * RW + tj + RX] : 0u);
       if (inb && (ab_ & 1u))
         live = (GNCA_ABLATE & kAblFire) ? ((cell & 1) != 0)
                                         : fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step,
@@ -500,6 +723,10 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       }
     }
     if (lane == 0) cnt[s] = nl;
+    if constexpr (FOLD) {   // this tile's slot is complete: the finalizers may read it
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     if (GNCA_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO);
   };
 
@@ -508,7 +735,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   // Prologue (what a small batch's launch waits out): the first tile's DMA, the preparer's planes of
   // that tile, then every weight load of this thread in flight together, then the weight images'
   // splits and LDS stores (B=8 72^2 K1: 20.0 -> 19.8 us; the preparer after the weight loads 22.3 us)
-  if (tile < t_end) issue_dma(tile, wave, NW);
+  if (!FOLD && tile < t_end) issue_dma(tile, wave, NW);
   PROF_MARK(0);   // (prologue) first tile's DMA issue
   if (wave == PW && tile < t_end) prep(tile, 0);
   PROF_MARK(3);   // (prologue) first tile's prep
@@ -534,6 +761,9 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     for (int e = tid; e < 16 * (PSTR - RHW); e += NT) xs[(e / (PSTR - RHW)) * PSTR + RHW + e % (PSTR - RHW)] = 0.f;
   }
   PROF_MARK(2);   // (prologue) weight image copy / fill issue
+  if constexpr (FOLD) {   // the first tile's region: finalized by every wave (nothing to wait for)
+    if (tile < t_end) finalize(tile, 0, 1, false, 0, 0);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PROF_MARK(1);   // (prologue) wait for the DMA, images and weight loads
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch; the
@@ -569,6 +799,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   // -> LDS-DMA of tile t+1's channel planes -> wait -> barrier.  The per-tile planes and the
   // compaction run on the preparer wave beside the other waves' groups instead of between them.
   int par = 0;
+  int iter = 0;
   while (tile < t_end) {
     PROF_MARK(7);
     const int nxt = next_active(tile + per_x);
@@ -1005,7 +1236,10 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     // The wave whose pull failed first (q == qend: the counter hands out consecutive values) stages
     // the next tile as soon as every group is past its staged-plane reads, while the other waves
     // still run their last groups' MFMAs and stores.
-    if (q >= qend && q < qend + GNCA_DMA_WAVES && nxt < t_end) {
+    if constexpr (FOLD) {
+      // every wave: the next tile's region finalized into the staging buffer (+ its cells into xo)
+      if (nxt < t_end) finalize(nxt, par ^ 1, iter + 2, true, qend, xbase);
+    } else if (q >= qend && q < qend + GNCA_DMA_WAVES && nxt < t_end) {
       while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xbase < qend)
         __builtin_amdgcn_s_sleep(1);
       issue_dma(nxt, q - qend, GNCA_DMA_WAVES);
@@ -1026,6 +1260,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     PROF_MARK(5);   // per-tile reduction
     tile = nxt;
     par ^= 1;
+    ++iter;
   }
   PROF_STORE_W03;
   GNCA_STAMP_END(a.stamps);

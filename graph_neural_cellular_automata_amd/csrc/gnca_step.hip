@@ -171,6 +171,24 @@ struct K1Args {
   uint32_t flags;
   uint64_t* stamps;    // measurement only (null in product launches): per-workgroup wall-clock stamps
   const char* wimg;    // split K1: the weight images built once per rollout (gnca_ks_images), or null
+  // The fold (rollout mode, gnca_k1_split<..., FOLD = true>): this launch also FINISHES the previous
+  // step.  Each tile's staged region is x = finalize(xp, dxp) (GroupNorm with the previous step's
+  // partials, tanh * gain, residual, post-update alpha gate: K2's arithmetic) instead of an LDS-DMA
+  // copy of `x`; the tile's interior of that state goes to xo; the pre-update masks come from the
+  // finalized alpha instead of `alive`.  The previous step's compact update field: dxp / rmaskp /
+  // rprep / dxap / statsp (written by the previous K1 launch, the same layout as out / rmask / rpre
+  // / dxa / stats).
+  const float* xp;
+  float* xo;
+  const float* dxp;
+  const uint64_t* rmaskp;
+  const uint32_t* rprep;
+  const float* dxap;
+  const double* statsp;
+  const float* gamma;
+  const float* beta;
+  float gain, eps;
+  int use_gn, nst;     // nst: GroupNorm partial pairs per sample (tps x waves)
   int odl[GNCA_MAX_OFFSETS];   // gather source delta in the staged region: dy*RW + dx (pad: dy*RW)
 };
 
@@ -179,6 +197,43 @@ struct K1Args {
 // and every VALU instruction costs fp32 MFMA issue time on the shared datapath).  Not inline asm:
 // hipcc does not insert the MFMA-result read hazard wait states around an asm statement.
 __device__ __forceinline__ float relu_nan(float v) { return __builtin_elementwise_maximum(v, 0.f); }
+
+// ------------------------------------------------------------------------------------------
+// The step's finalize arithmetic (ncagraph.py:153-166: GroupNorm, tanh * update_gain, residual,
+// post-update alpha gate), shared by K2 and the fold K1 (gnca_k1_split<..., FOLD>) so that both
+// produce the same bits.
+// ------------------------------------------------------------------------------------------
+constexpr float kL2E2 = 2.8853900817779268f;   // 2 / ln 2
+
+// per-sample mean / rstd of GroupNorm(1, C) from the fixed-order fp64 sums (t1 = sum, t2 = sum of
+// squares over n = C*H*W values, the zeros of masked cells included)
+__device__ __forceinline__ void fin_mu_rs(double t1, double t2, double n, float eps, float* mu, float* rs) {
+  const double m = t1 / n;
+  double var = t2 / n - m * m;
+  if (var < 0.0) var = 0.0;
+  *mu = (float)m;
+  *rs = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// a non-alpha channel's folded constants: x + tanh(z) * gain = (x + gain) - 2 gain / (2^(z 2 log2 e) + 1)
+// with z = GN(d) = d * gamma rs + (beta - mu gamma rs): sc = 2 log2(e) gamma rs, sh = 2 log2(e) (beta - mu gamma rs)
+__device__ __forceinline__ void fin_consts(float gam, float bet, float mu, float rs, bool gn, float* sc, float* sh) {
+  const float gr = gn ? gam * rs : 1.f;
+  *sc = gr * kL2E2;
+  *sh = (gn ? fmaf(-mu, gr, bet) : 0.f) * kL2E2;
+}
+
+// the update of one non-alpha value: (x + gain) + (-2 gain) / (2^(d sc + sh) + 1), g2 = -2 gain
+__device__ __forceinline__ float k2_update(float x, float d, float sc, float sh, float gain, float g2) {
+  return fmaf(g2, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(fmaf(d, sc, sh)) + 1.f), x + gain);
+}
+
+// the updated alpha x~_3 = x_3 + tanh(GN(d)) * gain (as the backward's BA: the same gate bits)
+__device__ __forceinline__ float fin_alpha(float xa, float d, float mu, float rs, float g3, float b3, float gain,
+                                           bool gn) {
+  if (gn) d = (d - mu) * rs * g3 + b3;
+  return xa + fast_tanh(d) * gain;
+}
 
 
 }  // namespace gnca
@@ -890,11 +945,6 @@ __device__ __forceinline__ int k2_sample(int j, int B, int zigzag) {
 // the band needs first (GroupNorm partials, alpha rows, gamma/beta and the first KU main items)
 // is issued before the first barrier: a small-batch launch waits out one memory latency, not
 // one per phase.
-// K2's update of one non-alpha value: x + tanh(GN(d)) * gain with GN and the tanh's 2/ln2 folded
-// into (sc, sh) per channel: (x + gain) + (-2 gain) / (2^(d sc + sh) + 1)
-__device__ __forceinline__ float k2_update(float x, float d, float sc, float sh, float gain, float g2) {
-  return fmaf(g2, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(fmaf(d, sc, sh)) + 1.f), x + gain);
-}
 
 template <int V, bool COMPACT>
 __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_norm) {
@@ -983,12 +1033,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
     if (gn) {
       double t1, t2;
       wave_sum2(a.stats + (size_t)b * a.nst * 2, a.nst, &t1, &t2);
-      const double n = (double)C * (double)HW;
-      const double m = t1 / n;
-      double var = t2 / n - m * m;
-      if (var < 0.0) var = 0.0;
-      mu = (float)m;
-      rs = (float)(1.0 / sqrt(var + (double)a.eps));
+      fin_mu_rs(t1, t2, (double)C * (double)HW, a.eps, &mu, &rs);
     }
     if (lane == 0) {
       float amn = 0.f, amx = 0.f;
@@ -1010,19 +1055,11 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   // with z = GN(d) = d * gamma rs + (beta - mu gamma rs); per channel k2s[c] = 2 log2(e) gamma rs,
   // k2s[32 + c] = 2 log2(e) (beta - mu gamma rs) (written here, read after the next barrier)
   float* k2s = sh_norm + 4 + 64;
-  constexpr float kL2E2 = 2.8853900817779268f;   // 2 / ln 2
-  if (tid < C) {
-    const float gr = gn ? gsh[tid] * rs : 1.f;
-    k2s[tid] = gr * kL2E2;
-    k2s[32 + tid] = (gn ? fmaf(-mu, gr, gsh[32 + tid]) : 0.f) * kL2E2;
-  }
+  if (tid < C) fin_consts(gsh[tid], gsh[32 + tid], mu, rs, gn, &k2s[tid], &k2s[32 + tid]);
   const float g2 = -2.f * a.gain;
 
   // (3) updated alpha over band + halo, then the post-update alive mask (3x3 max-pool, -inf pad)
-  auto alpha_at = [&](float xa, float d) {
-    if (gn) d = (d - mu) * rs * g3 + b3;
-    return xa + fast_tanh(d) * a.gain;   // as the backward's BA (the same gate bits)
-  };
+  auto alpha_at = [&](float xa, float d) { return fin_alpha(xa, d, mu, rs, g3, b3, a.gain, gn); };
   // compact field: K1 writes the alpha plane for live cells only; a dead cell's update is 0 (its
   // row's live mask, already in LDS for the band rows and the halo rows)
   auto live_at = [&](int e) {
@@ -1344,20 +1381,24 @@ struct Variant {
   int NT;                            // threads per workgroup
   int split;                         // 1: gnca_k1_split, 2: gnca_k1_split32 (bf16 MFMA on exact 3-way splits)
   int lds_split;                     // its LDS bytes (compile-time layout)
+  const void* fold_fn;               // the same K1 that also finishes the previous step (rollouts), or null
 };
 
-#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0}
+#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0, nullptr}
 #define GNCA_SV(th, tw, ry, rx, ku) \
   {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
-   ks_layout<th, tw, ry, rx>().total}
+   ks_layout<th, tw, ry, rx>().total, nullptr}
+#define GNCA_SVF(th, tw, ry, rx, ku) \
+  {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
+   ks_layout<th, tw, ry, rx>().total, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku, true>)}
 #define GNCA_S32V(th, tw, ry, rx, ku) \
   {32, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split32<th, tw, ry, rx, ku>), 512, 2, \
-   ks32_layout<th, tw, ry, rx>().total}
+   ks32_layout<th, tw, ry, rx>().total, nullptr}
 static const Variant kVariants[] = {
     // 16 channels, hidden 128, bf16 MFMA on exact 3-way splits (gnca_k1_split.h), compile-time
     // geometry: list order is the large-batch preference (24x36: the largest tiles whose halo fits
     // LDS, 1.6x halo re-read); 8x24 / 8x20 serve small batches and the trainer's 40^2 canvas
-    GNCA_SV(24, 36, 4, 4, 8),
+    GNCA_SVF(24, 36, 4, 4, 8),   // + the fold variant (large-batch rollouts: one K1 launch per step)
     GNCA_SV(36, 24, 4, 4, 8),
     GNCA_SV(24, 24, 4, 4, 8),
     GNCA_SV(8, 24, 4, 4, 8),
@@ -1376,6 +1417,7 @@ static const Variant kVariants[] = {
 };
 #undef GNCA_GV
 #undef GNCA_SV
+#undef GNCA_SVF
 #undef GNCA_S32V
 
 static const Variant* find_variant(int C, int Hd) {
@@ -1400,6 +1442,11 @@ struct Plan {
   // workspace carve (bytes)
   size_t off_dx, off_stats, off_mm, off_offw, off_alive, off_rmask, off_rpre, off_dxa, off_wimg, ws_bytes;
   bool compact_ok;   // the rollout's compact update field (the bf16-split K1s, large batches)
+  // the fold (rollouts of a fold-capable K1 on the compact field): K1 of step t also finishes step
+  // t - 1, so the compact field (dx, row tables, alpha plane, partials) is double-buffered by the
+  // parity of the global step index: set 1 at off_*2
+  bool fold_ok;
+  size_t off_dx2, off_stats2, off_rmask2, off_rpre2, off_dxa2;
 };
 
 static int max_lds_bytes() { return 160 * 1024; }
@@ -1557,6 +1604,16 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->off_dxa = carve(P->compact_ok ? (size_t)d->B * d->H * d->W * sizeof(float) : 0);
   // the rollout's weight images of the 16-channel split K1 (built once per rollout, gnca_ks_images)
   P->off_wimg = carve(P->var->split == 1 ? (size_t)(ks_layout<24, 36, 4, 4>().total - ks_layout<24, 36, 4, 4>().w1) : 0);
+  // the fold: a fold-capable K1 on the compact field, thresholds that allow the alive hand-over
+  // (0 <= alpha_thr <= graph_alpha_thr), 32-bit packed-field offsets; the second set of
+  // the compact field (each field + 256 B: the finalizer's quad reads may touch one float past it)
+  P->fold_ok = P->compact_ok && P->var->fold_fn != nullptr && P->graph_on && P->k == P->var->KU &&
+               d->alpha_thr >= 0.f && d->graph_alpha_thr >= d->alpha_thr && n < (size_t)1 << 31;
+  P->off_dx2 = carve(P->fold_ok ? n * 4 + 256 : 0);
+  P->off_stats2 = carve(P->fold_ok ? (size_t)P->total_tiles * P->ppt * 2 * sizeof(double) : 0);
+  P->off_rmask2 = carve(P->fold_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint64_t) : 0);
+  P->off_rpre2 = carve(P->fold_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint32_t) : 0);
+  P->off_dxa2 = carve(P->fold_ok ? (size_t)d->B * d->H * d->W * sizeof(float) : 0);
   P->ws_bytes = o;
   if (P->need_k0) {
     const size_t k0 = ((size_t)d->C * d->H + d->C + d->d_model + P->k) * sizeof(double);
@@ -1702,13 +1759,32 @@ static bool weights_ok(const gnca_step_desc* d, const gnca_weights* w, bool msg_
   return true;
 }
 
+// The update field of one step in the workspace: set 0, or (the fold's double buffer) set 1.
+struct FieldSet {
+  float* dx;
+  double* stats;
+  uint64_t* rmask;
+  uint32_t* rpre;
+  float* dxa;
+};
+static FieldSet field_set(const Plan& P, char* wsb, int set) {
+  if (set == 0)
+    return {reinterpret_cast<float*>(wsb + P.off_dx), reinterpret_cast<double*>(wsb + P.off_stats),
+            reinterpret_cast<uint64_t*>(wsb + P.off_rmask), reinterpret_cast<uint32_t*>(wsb + P.off_rpre),
+            reinterpret_cast<float*>(wsb + P.off_dxa)};
+  return {reinterpret_cast<float*>(wsb + P.off_dx2), reinterpret_cast<double*>(wsb + P.off_stats2),
+          reinterpret_cast<uint64_t*>(wsb + P.off_rmask2), reinterpret_cast<uint32_t*>(wsb + P.off_rpre2),
+          reinterpret_cast<float*>(wsb + P.off_dxa2)};
+}
+
 // alive_in / alive_out (rollout only): the previous step's K2 hands this step's K1 its pre-update
-// masks as bytes, so K1 skips the alpha halo and the 3x3 max-pools.
+// masks as bytes, so K1 skips the alpha halo and the 3x3 max-pools.  set: the update
+// field set (the fold rollout alternates sets 0 / 1 by step parity; everything else uses 0).
 static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float* x, float* x_out,
                      const void* fire, float* attn, void* ws, size_t ws_bytes, hipStream_t st,
                      uint32_t phases = GNCA_PHASE_ALL, const uint8_t* active = nullptr,
                      bool alive_in = false, bool alive_out = false, bool compact = false,
-                     uint64_t* stamps = nullptr, int stamp_cap = 0, const char* wimg = nullptr) {
+                     uint64_t* stamps = nullptr, int stamp_cap = 0, const char* wimg = nullptr, int set = 0) {
   Plan P;
   if (!make_plan(d, false, &P)) {
     if (d && d->C >= 4 && d->hidden > 0 && !find_variant(d->C, d->hidden)) return GNCA_ERR_UNSUPPORTED;
@@ -1722,6 +1798,8 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   if (want_attn && !attn) return GNCA_ERR_INVALID;
   if (!ws || ws_bytes < P.ws_bytes) return GNCA_ERR_WORKSPACE;
   char* wsb = reinterpret_cast<char*>(ws);
+  if (set != 0 && !P.fold_ok) return GNCA_ERR_INVALID;
+  const FieldSet fs = field_set(P, wsb, set);
   int rc;
   if ((phases & GNCA_PHASE_K0) && P.need_k0 && (rc = launch_k0(d, w, P, x, wsb, st)) != GNCA_OK)
     return rc;
@@ -1731,8 +1809,9 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
       return GNCA_ERR_HIP;
   }
   K1Args k1;
-  float* dx = reinterpret_cast<float*>(wsb + P.off_dx);
+  float* dx = fs.dx;
   fill_k1(k1, d, w, P, x, dx, fire, want_attn ? attn : nullptr, wsb);
+  k1.stats = fs.stats;
   k1.active = active;
   uint8_t* alive = reinterpret_cast<uint8_t*>(wsb + P.off_alive);
   // the split K1s always read the masks as bytes (their preparer wave builds the planes from
@@ -1748,9 +1827,9 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   }
   // compact update field (rollout mode): K1 packs the live cells' dx per tile, K2 unpacks them
   compact = compact && P.compact_ok && !active && !want_attn;
-  uint64_t* rmask = reinterpret_cast<uint64_t*>(wsb + P.off_rmask);
-  uint32_t* rpre = reinterpret_cast<uint32_t*>(wsb + P.off_rpre);
-  float* dxa = reinterpret_cast<float*>(wsb + P.off_dxa);
+  uint64_t* rmask = fs.rmask;
+  uint32_t* rpre = fs.rpre;
+  float* dxa = fs.dxa;
   if (compact) {
     k1.rmask = rmask;
     k1.rpre = rpre;
@@ -1767,7 +1846,7 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   K2Args k2;
   memset(&k2, 0, sizeof(k2));
   k2.x = x; k2.dx = dx; k2.out = x_out;
-  k2.stats = reinterpret_cast<const double*>(wsb + P.off_stats);
+  k2.stats = fs.stats;
   k2.use_gn = (d->flags & GNCA_USE_GROUPNORM) ? 1 : 0;
   k2.gamma = w->gn_weight; k2.beta = w->gn_bias;
   k2.attn = (want_attn && P.graph_on) ? attn : nullptr;
@@ -1800,6 +1879,46 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
                       : ((d->W & 3) == 0 ? gnca_k2_finalize<4, false> : gnca_k2_finalize<1, false>);
   hipLaunchKernelGGL(k2fn, dim3(compact ? P.total2_c : P.total2), dim3(kThreads),
                      compact ? P.lds2_c : P.lds2, st, k2);
+  return check_launch();
+}
+
+// One fold K1 launch of a rollout (P.fold_ok): step `d` (offsets, rng_step) on the state
+// finalize(xp, field set 1 - set) — written to xo for every tile's own cells — with its update field
+// into set `set`.
+static int fold_k1(const gnca_step_desc* d, const gnca_weights* w, const Plan& P, const float* xp, float* xo,
+                   char* wsb, int set, hipStream_t st, uint64_t* stamps, int stamp_cap, const char* wimg) {
+  const FieldSet cur = field_set(P, wsb, set), prev = field_set(P, wsb, set ^ 1);
+  K1Args k1;
+  fill_k1(k1, d, w, P, xp, cur.dx, nullptr, nullptr, wsb);
+  k1.stats = cur.stats;
+  k1.rmask = cur.rmask;
+  k1.rpre = cur.rpre;
+  k1.dxa = cur.dxa;
+  k1.xp = xp;
+  k1.xo = xo;
+  k1.dxp = prev.dx;
+  k1.rmaskp = prev.rmask;
+  k1.rprep = prev.rpre;
+  k1.dxap = prev.dxa;
+  k1.statsp = prev.stats;
+  k1.use_gn = (d->flags & GNCA_USE_GROUPNORM) ? 1 : 0;
+  k1.gamma = w->gn_weight;
+  k1.beta = w->gn_bias;
+  k1.gain = d->update_gain;
+  k1.eps = d->gn_eps;
+  k1.nst = P.tps * P.ppt;
+  k1.wimg = wimg;
+  k1.stamps = stamps;
+  const int occ = occupancy(P.var->fold_fn, P.lds1, P.var->NT);
+  long grid = std::min<long>((long)device_cus() * occ, P.total_tiles);
+  if (grid < 1) grid = 1;
+  if (stamps && grid > stamp_cap) return GNCA_ERR_INVALID;
+  void* args[] = {&k1};
+  const hipError_t e = hipLaunchKernel(P.var->fold_fn, dim3((unsigned)grid), dim3(P.var->NT), args, P.lds1, st);
+  if (e != hipSuccess) {
+    g_last_hip = (int)e;
+    return GNCA_ERR_HIP;
+  }
   return check_launch();
 }
 
@@ -1845,7 +1964,7 @@ static void sub_desc(const gnca_step_desc* d, int sub, int nsub, gnca_step_desc*
 static int rollout_subs(const gnca_step_desc* d) {
   if (kRolloutSubs < 2 || !d || d->B < kRolloutSubs) return 1;
   Plan P;
-  if (!make_plan(d, false, &P) || P.var->split != 1 || !P.compact_ok) return 1;
+  if (!make_plan(d, false, &P) || P.var->split != 1 || !P.compact_ok || P.fold_ok) return 1;
   for (int s = 0; s < kRolloutSubs; ++s) {
     gnca_step_desc sd;
     int b0;
@@ -1939,7 +2058,8 @@ int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* 
   else
     snprintf(name, (size_t)n, "gnca_k1_update<%d,%d,%d,%d,%d,%d,%d,%d>", v->CP, v->HDP, v->TH, v->TW, v->RY, v->RX,
              v->KU, v->NT);
-  if (arith) *arith = (v->split ? 1 : 0) | (P.compact_ok ? 2 : 0) | (rollout_subs(desc) > 1 ? 4 : 0);
+  if (arith) *arith = (v->split ? 1 : 0) | (P.compact_ok ? 2 : 0) | (rollout_subs(desc) > 1 ? 4 : 0) |
+                      (P.fold_ok ? 8 : 0);
   return GNCA_OK;
 }
 
@@ -2042,7 +2162,11 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
                         void* ws, size_t ws_bytes, void* stream, uint64_t* stamps, int stamp_cap,
                         uint32_t flags) {
   if (!desc || steps < 0 || !x || !x_final || !scratch) return GNCA_ERR_INVALID;
-  if (flags & ~(uint32_t)(GNCA_ROLLOUT_ALIVE_IN | GNCA_ROLLOUT_ALIVE_OUT)) return GNCA_ERR_INVALID;
+  if (flags & ~(uint32_t)(GNCA_ROLLOUT_ALIVE_IN | GNCA_ROLLOUT_ALIVE_OUT | GNCA_ROLLOUT_PENDING_IN |
+                          GNCA_ROLLOUT_PENDING_OUT))
+    return GNCA_ERR_INVALID;
+  if ((flags & GNCA_ROLLOUT_ALIVE_IN) && (flags & GNCA_ROLLOUT_PENDING_IN)) return GNCA_ERR_INVALID;
+  if ((flags & GNCA_ROLLOUT_ALIVE_OUT) && (flags & GNCA_ROLLOUT_PENDING_OUT)) return GNCA_ERR_INVALID;
   if (desc->fire_mode != GNCA_FIRE_NONE && desc->fire_mode != GNCA_FIRE_HASH) return GNCA_ERR_INVALID;
   if (x == x_final || x == scratch || x_final == scratch) return GNCA_ERR_INVALID;
   // a zero-step piece of a rollout issued in pieces would have to order its copy after the other
@@ -2063,7 +2187,12 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
   const bool hand_alive = desc->alpha_thr >= 0.f && desc->graph_alpha_thr >= desc->alpha_thr;
   if ((flags & (GNCA_ROLLOUT_ALIVE_IN | GNCA_ROLLOUT_ALIVE_OUT)) && !hand_alive) return GNCA_ERR_INVALID;
   const bool in0 = (flags & GNCA_ROLLOUT_ALIVE_IN) != 0, out_last = (flags & GNCA_ROLLOUT_ALIVE_OUT) != 0;
+  const bool pend_in = (flags & GNCA_ROLLOUT_PENDING_IN) != 0, pend_out = (flags & GNCA_ROLLOUT_PENDING_OUT) != 0;
   const int nsub = rollout_subs(&dt);
+  Plan PF;
+  if (!make_plan(&dt, false, &PF)) return GNCA_ERR_INVALID;
+  const bool fold = PF.fold_ok && nsub == 1;
+  if ((pend_in || pend_out) && !fold) return GNCA_ERR_INVALID;
   // the 16-channel split K1's weight images, once for the whole rollout (every K1 launch then copies
   // them into LDS with LDS-DMA instead of loading, splitting and storing the fp32 weights)
   const char* wimg = nullptr;
@@ -2077,7 +2206,7 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
       // a continuation piece (ALIVE_IN) reuses the images its first piece built in the same workspace
       // (rebuilding them here could overwrite them under the other sub-batch stream's K1)
       char* dst = reinterpret_cast<char*>(ws) + P0.off_wimg;
-      if (!in0) {
+      if (!in0 && !pend_in) {
         K1Args ka;
         fill_k1(ka, &d0, w, P0, x, nullptr, nullptr, nullptr, reinterpret_cast<char*>(ws));
         hipLaunchKernelGGL(gnca_ks_images, dim3(1), dim3(512), 0, st, ka, dst);
@@ -2086,6 +2215,43 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
       }
       wimg = dst;
     }
+  }
+  if (fold) {
+    // The fold: K1 of step t also finishes step t - 1 (one launch per step); the update field of
+    // global step g lives in set g & 1.  State S_t = the input of step t: S_0 = x (or, PENDING_IN,
+    // finalize(x, the pending field), written by the first K1); K1 of step t >= 1 writes S_t; the
+    // last step is finished by K2 into x_final (or, PENDING_OUT, left pending: S_{T-1} is x_final).
+    if (!weights_ok(&dt, w, false, PF)) return GNCA_ERR_INVALID;
+    if (!ws || ws_bytes < PF.ws_bytes) return GNCA_ERR_WORKSPACE;
+    char* wsb = reinterpret_cast<char*>(ws);
+    const int T = steps;
+    const int last = pend_out ? T - 1 : T;   // the state that lands in x_final
+    auto buf = [&](int t) -> float* { return ((last - t) % 2 == 0) ? x_final : scratch; };
+    auto state = [&](int t) -> const float* { return (t == 0 && !pend_in) ? x : buf(t); };
+    for (int t = 0; t < T; ++t) {
+      dt.rng_step = desc->rng_step + t;
+      if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(dt.offsets, offsets + (size_t)t * 2 * k, 2 * k);
+      const int set = (int)(dt.rng_step & 1);
+      uint64_t* sk = stamps ? stamps + (size_t)t * 4 * stamp_cap : nullptr;
+      int rc;
+      if (t == 0 && !pend_in)
+        rc = step_impl(&dt, w, x, x_final, nullptr, nullptr, ws, ws_bytes, st, GNCA_PHASE_K0 | GNCA_PHASE_K1,
+                       nullptr, in0, false, true, sk, stamp_cap, wimg, set);
+      else
+        rc = fold_k1(&dt, w, PF, t == 0 ? x : state(t - 1), buf(t), wsb, set, st, sk, stamp_cap, wimg);
+      if (rc != GNCA_OK) return rc;
+    }
+    if (pend_out) {   // the pending state S_{T-1} must be in x_final (T == 1: it is the input x)
+      if (T == 1 && !pend_in &&
+          hipMemcpyAsync(x_final, x, (size_t)desc->B * desc->C * desc->H * desc->W * sizeof(float),
+                         hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return GNCA_ERR_HIP;
+      return GNCA_OK;
+    }
+    // the last step's finish: K2 on the compact field of step T - 1
+    return step_impl(&dt, w, state(T - 1), x_final, nullptr, nullptr, ws, ws_bytes, st, GNCA_PHASE_K2, nullptr,
+                     false, out_last, true, stamps ? stamps + (size_t)(T - 1) * 4 * stamp_cap : nullptr, stamp_cap,
+                     wimg, (int)(dt.rng_step & 1));
   }
   if (nsub == 1) {
     const float* src = x;

@@ -121,7 +121,9 @@ size_t gnca_workspace_bytes(const gnca_step_desc* desc);
  * (v_mfma_f32_*_f32), 1 = bf16 MFMA on exact 3-way splits of the fp32 operands (6 products per
  * fp32 product, gnca_k1_split.h), plus 2 when a rollout of this shape uses the compact update field
  * (GNCA_PHASE_COMPACT), plus 4 when a rollout of this shape runs as 2 concurrent sub-batches (one
- * stream each: one sub-batch's K2 beside the other's K1; see gnca_rollout_f32).  Host-only.
+ * stream each: one sub-batch's K2 beside the other's K1; see gnca_rollout_f32), plus 8 when a
+ * rollout of this shape folds each step's finish (GroupNorm, tanh, residual, alpha gate) into the
+ * next step's K1 (one K1 launch per step and one K2 at the end).  Host-only.
  * Returns GNCA_OK or GNCA_ERR_INVALID. */
 int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* arith);
 
@@ -208,6 +210,21 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
  */
 #define GNCA_ROLLOUT_ALIVE_IN  (1u << 0)
 #define GNCA_ROLLOUT_ALIVE_OUT (1u << 1)
+/*
+ * Rollouts that fold each step's finish into the next step's K1 (gnca_k1_variant's arith bit 8: one
+ * K1 launch per step, one K2 at the end) can hand the LAST step over unfinished instead, which
+ * saves the K2 and the next piece's plain first K1:
+ *   GNCA_ROLLOUT_PENDING_OUT  the last step is left pending: x_final receives the state BEFORE the
+ *                             last step and `ws` holds that step's update field
+ *   GNCA_ROLLOUT_PENDING_IN   x is such a state and `ws` the pending field of the previous call
+ *                             (same desc shape, workspace and stream; desc->rng_step continues the
+ *                             previous call's: the field's buffer is chosen by the step's parity)
+ * A piece chain PENDING_OUT, PENDING_IN|PENDING_OUT, ..., PENDING_IN computes exactly the one-call
+ * rollout.  GNCA_ERR_INVALID when the rollout does not fold, or combined with ALIVE_IN / ALIVE_OUT
+ * on the same side.
+ */
+#define GNCA_ROLLOUT_PENDING_IN  (1u << 2)
+#define GNCA_ROLLOUT_PENDING_OUT (1u << 3)
 int gnca_rollout_ex_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
                         const int8_t* offsets, const float* x, float* x_final, float* scratch,
                         void* ws, size_t ws_bytes, uint32_t flags, void* stream);

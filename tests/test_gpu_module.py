@@ -196,6 +196,7 @@ def test_compact_rollout_equals_dense_steps(dev, graph):
 
     name, arith = S.k1_variant(desc(0))
     assert arith == "bf16x6", name
+    assert S.rollout_fold(desc(0)) == graph   # the graph rollout folds each finish into the next K1
     r = S.rollout(desc(0), w, x.contiguous(), steps, offs)
     cur = x
     for t in range(steps):
@@ -428,29 +429,26 @@ def test_masked_step_many_tiles_per_workgroup(dev):
 
 
 def test_subbatch_rollout_and_pieces_bitwise(dev):
-    """A large-batch rollout runs as 2 sub-batches on two streams (one sub-batch's K2 beside the
-    other's K1): bitwise the states of repeated single steps; and a rollout issued in pieces with the
-    alive masks handed over through the workspace (gnca_rollout_ex_f32 ALIVE_OUT / ALIVE_IN) is
-    bitwise the one-call rollout."""
+    """A large-batch rollout that does not fold (the classic step) runs as 2 sub-batches on two
+    streams (one sub-batch's K2 beside the other's K1): bitwise the states of repeated single steps;
+    and a rollout issued in pieces with the alive masks handed over through the workspace
+    (gnca_rollout_ex_f32 ALIVE_OUT / ALIVE_IN) is bitwise the one-call rollout."""
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
     m = _trained_like(dev, seed=9)
-    B, steps = 192, 5
+    B, steps = 384, 5
     x = _state(B, 16, 72, 72, dev, seed=29)
-    random.seed(19)
-    offs = [random.sample(m.graph.offsets, 8) for _ in range(steps)]
+    offs = [[] for _ in range(steps)]
     w, keep = S.make_weights(dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
                                   b1=m.update_net[0].bias, w2=m.update_net[2].weight,
-                                  gn_weight=m.norm.weight, gn_bias=m.norm.bias,
-                                  **m.graph.weight_tensors()))
+                                  gn_weight=m.norm.weight, gn_bias=m.norm.bias))
 
     def desc(t):
-        return S.make_desc(B=B, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[t],
-                           flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
-                           update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
-                           fire_mode=L.FIRE_HASH, rng_seed=3, rng_step=t, sample_base=7)
+        return S.make_desc(B=B, C=16, H=72, W=72, hidden=128, d_model=16, offsets=[],
+                           flags=L.USE_GROUPNORM, update_gain=0.05, alpha_thr=0.12, message_gain=0.25,
+                           fire_rate=0.5, fire_mode=L.FIRE_HASH, rng_seed=3, rng_step=t, sample_base=7)
 
-    assert S.rollout_subs(desc(0)) == 2
+    assert S.rollout_subs(desc(0)) == 2 and not S.rollout_fold(desc(0))
     r = S.rollout(desc(0), w, x.contiguous(), steps, offs)
     cur = x
     for t in range(steps):
@@ -462,8 +460,7 @@ def test_subbatch_rollout_and_pieces_bitwise(dev):
     a, b2, scratch = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
     st = torch.cuda.current_stream().cuda_stream
     for (s0, n, src, dst, fl) in ((0, 2, x, a, L.ROLLOUT_ALIVE_OUT), (2, 3, a, b2, L.ROLLOUT_ALIVE_IN)):
-        flat = [v for o in offs[s0:s0 + n] for p in o for v in p]
-        arr = (ctypes.c_int8 * len(flat))(*flat)
+        arr = None
         L.check(lib.gnca_rollout_ex_f32(ctypes.byref(desc(s0)), ctypes.byref(w), n, arr, src.data_ptr(),
                                         dst.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(), fl, st),
                 "gnca_rollout_ex_f32")
@@ -484,3 +481,72 @@ def test_make_weights_cache_rejects_non_contiguous_at_cached_address(dev):
     assert any(k.data_ptr() == w_b.w2 and torch.equal(k, v) for k in keep)
     with pytest.raises(TypeError):
         S.make_weights({"w2": t.view(torch.int32)})
+
+
+def test_fold_rollout_pieces_bitwise(dev):
+    """The fold (each step's finish inside the next step's K1, one launch per step): a rollout issued
+    as a chain of pieces that hand the last step over unfinished (PENDING_OUT / PENDING_IN, piece
+    sizes 1, 1, 2, 3 and a single one-step piece chain) is bitwise the one-call rollout and the
+    repeated unfused single steps; bad flag combinations are rejected."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    m = _trained_like(dev, seed=12)
+    B, steps = 160, 7
+    x = _state(B, 16, 72, 72, dev, seed=31)
+    random.seed(23)
+    offs = [random.sample(m.graph.offsets, 8) for _ in range(steps)]
+    w, keep = S.make_weights(dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
+                                  b1=m.update_net[0].bias, w2=m.update_net[2].weight,
+                                  gn_weight=m.norm.weight, gn_bias=m.norm.bias,
+                                  **m.graph.weight_tensors()))
+
+    def desc(t):
+        return S.make_desc(B=B, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[t],
+                           flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                           update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                           fire_mode=L.FIRE_HASH, rng_seed=11, rng_step=t, sample_base=3)
+
+    assert S.rollout_fold(desc(0)) and S.rollout_subs(desc(0)) == 1
+    one = S.rollout(desc(0), w, x.contiguous(), steps, offs)
+    cur = x
+    for t in range(steps):
+        cur, _ = S.step(desc(t), w, cur)
+    assert torch.equal(one, cur)
+    lib = L.load()
+    ws = S.workspace(desc(0), dev)
+    st = torch.cuda.current_stream().cuda_stream
+    scratch = torch.empty_like(x)
+
+    def run(sizes):
+        src, s0 = x.contiguous(), 0
+        outs = [torch.empty_like(x), torch.empty_like(x)]
+        for i, n in enumerate(sizes):
+            fl = (L.ROLLOUT_PENDING_IN if i > 0 else 0) | (L.ROLLOUT_PENDING_OUT if i + 1 < len(sizes) else 0)
+            flat = [v for o in offs[s0:s0 + n] for p in o for v in p]
+            arr = (ctypes.c_int8 * len(flat))(*flat)
+            dst = outs[i % 2]
+            L.check(lib.gnca_rollout_ex_f32(ctypes.byref(desc(s0)), ctypes.byref(w), n, arr, src.data_ptr(),
+                                            dst.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(), fl, st),
+                    "gnca_rollout_ex_f32")
+            src, s0 = dst, s0 + n
+        return src
+
+    assert torch.equal(run([1, 1, 2, 3]), one)
+    assert torch.equal(run([4, 3]), one)
+    assert torch.equal(run([6, 1]), one)
+    # PENDING with ALIVE on the same side, and PENDING on a rollout that does not fold: invalid
+    arr = (ctypes.c_int8 * 16)(*[v for p in offs[0] for v in p])
+    for fl in (L.ROLLOUT_PENDING_OUT | L.ROLLOUT_ALIVE_OUT, L.ROLLOUT_PENDING_IN | L.ROLLOUT_ALIVE_IN):
+        assert lib.gnca_rollout_ex_f32(ctypes.byref(desc(0)), ctypes.byref(w), 1, arr, x.data_ptr(),
+                                       scratch.data_ptr(), torch.empty_like(x).data_ptr(), ws.data_ptr(),
+                                       ws.numel(), fl, st) == -1
+    d8 = S.make_desc(B=8, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[0],
+                     flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                     update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                     fire_mode=L.FIRE_HASH, rng_seed=11)
+    assert not S.rollout_fold(d8)
+    x8 = x[:8].contiguous()
+    ws8 = S.workspace(d8, dev)
+    assert lib.gnca_rollout_ex_f32(ctypes.byref(d8), ctypes.byref(w), 1, arr, x8.data_ptr(),
+                                   torch.empty_like(x8).data_ptr(), torch.empty_like(x8).data_ptr(), ws8.data_ptr(),
+                                   ws8.numel(), L.ROLLOUT_PENDING_OUT, st) == -1
