@@ -359,7 +359,8 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   int* pdone = cnt + 5;
   int fbase = 0;
   constexpr int NQB = (NQ + 63) / 64, NFIN = 4 * NQB;
-  static_assert(!FOLD || (KU > 0 && C == 16), "the fold variant is the 16-channel graph K1");
+  // the fold reads the previous step's update field either compact (large batches: rmaskp != null)
+  // or dense NCHW with the dead cells' zeros (small batches)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   wg_stamp(a.stamps, 0);
@@ -458,8 +459,9 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     int gcol = j0 - RX - 4 + (lin ? lane : 0);
     gcol = gcol < 0 ? gcol + W : (gcol >= W ? gcol - W : gcol);
     const int txS = gcol / TW, tjS = gcol - txS * TW;
+    const bool cfield = a.rmaskp != nullptr;
     const float* xpa = a.xp + ((size_t)b * C + 3) * HW;
-    const float* dpa = a.dxap + (size_t)b * HW;
+    const float* dpa = cfield ? a.dxap + (size_t)b * HW : a.dxp + ((size_t)b * C + 3) * HW;
     const uint64_t* rmb = a.rmaskp + (size_t)b * a.tps * TH;
 #pragma unroll 1
     for (int r0 = 0; r0 < PBH; r0 += RB) {
@@ -473,12 +475,12 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         const int tyS = g / TH, tiS = g - tyS * TH;
         xv[u] = 0.f;
         dv[u] = 0.f;
-        mv[u] = 0ull;
+        mv[u] = ~0ull;   // dense field: every value is used (a dead cell's is 0)
         if (lin && r < PBH) {
           const size_t cell = (size_t)g * W + gcol;
           xv[u] = xpa[cell];
           dv[u] = dpa[cell];
-          mv[u] = rmb[(size_t)(tyS * a.tiles_x + txS) * TH + tiS];
+          if (cfield) mv[u] = rmb[(size_t)(tyS * a.tiles_x + txS) * TH + tiS];
         }
       }
 #pragma unroll
@@ -548,6 +550,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const float mu = fks[32], rs = fks[33], g3 = fks[34], b3 = fks[35];
     const bool gn = a.use_gn != 0;
     const float g2 = -2.f * a.gain;
+    const bool cfield = a.rmaskp != nullptr;
     bool waited = !wait_xsd;
 #pragma unroll 1
     for (;;) {
@@ -560,31 +563,42 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       int g = i0 - RY + vr, gc = j0 - RX + 4 * vq;
       g = g < 0 ? g + H : (g >= H ? g - H : g);
       gc = gc < 0 ? gc + W : (gc >= W ? gc - W : gc);
-      const int tyS = g / TH, tiS = g - tyS * TH, txS = gc / TW, tjS = gc - txS * TW;
-      const uint32_t tsrc = (uint32_t)(b * a.tps + tyS * a.tiles_x + txS);
-      const uint64_t m = a.rmaskp[(size_t)tsrc * TH + tiS];
-      const uint32_t pre = a.rprep[(size_t)tsrc * TH + tiS];
       const size_t cell = (size_t)g * W + gc;
       f4 xq[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         xq[u] = *reinterpret_cast<const f4*>(a.xp + ((size_t)b * C + 4 * cg + u) * HW + cell);
       f4 dqa = {0.f, 0.f, 0.f, 0.f};
-      if (cg == 0) dqa = *reinterpret_cast<const f4*>(a.dxap + (size_t)b * HW + cell);
-      // the quad's live cells are consecutive in the source tile's packed field: cell k's value (or,
-      // for a dead cell, the next live one's; never used) at rank r0 + (live cells before k)
-      const uint32_t bits = (uint32_t)(m >> tjS) & 15u;
-      const uint32_t r0 = tsrc * (uint32_t)(C * NCELL) + pre + (uint32_t)__popcll(m & ((1ull << tjS) - 1ull));
-      uint32_t off[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) off[k] = r0 + (uint32_t)__popc(bits & ((1u << k) - 1u));
       float dv[4][4];
+      uint32_t bits = 15u;   // dense field: every value is used (a dead cell's is 0)
+      if (cfield) {
+        const int tyS = g / TH, tiS = g - tyS * TH, txS = gc / TW, tjS = gc - txS * TW;
+        const uint32_t tsrc = (uint32_t)(b * a.tps + tyS * a.tiles_x + txS);
+        const uint64_t m = a.rmaskp[(size_t)tsrc * TH + tiS];
+        const uint32_t pre = a.rprep[(size_t)tsrc * TH + tiS];
+        if (cg == 0) dqa = *reinterpret_cast<const f4*>(a.dxap + (size_t)b * HW + cell);
+        // the quad's live cells are consecutive in the source tile's packed field: cell k's value
+        // (or, for a dead cell, the next live one's; never used) at rank r0 + (live cells before k)
+        bits = (uint32_t)(m >> tjS) & 15u;
+        const uint32_t r0 = tsrc * (uint32_t)(C * NCELL) + pre + (uint32_t)__popcll(m & ((1ull << tjS) - 1ull));
+        uint32_t off[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c = 4 * cg + u;
-        const float* fb = a.dxp + (size_t)c * NCELL;
+        for (int k = 0; k < 4; ++k) off[k] = r0 + (uint32_t)__popc(bits & ((1u << k) - 1u));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) dv[u][k] = c == 3 ? 0.f : fb[off[k]];
+        for (int u = 0; u < 4; ++u) {
+          const int c = 4 * cg + u;
+          const float* fb = a.dxp + (size_t)c * NCELL;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) dv[u][k] = c == 3 ? 0.f : fb[off[k]];
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const f4 d4 = *reinterpret_cast<const f4*>(a.dxp + ((size_t)b * C + 4 * cg + u) * HW + cell);
+          if (4 * cg + u == 3) dqa = d4;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) dv[u][k] = d4[k];
+        }
       }
       if (!waited) {
         while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xb < qe)
@@ -674,7 +688,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     constexpr bool SMALLT = NCH <= 4;
     constexpr int CUNR = SMALLT ? 4 : 1;
     uint32_t cab[SMALLT ? NCH : 1];
-    if constexpr (SMALLT) {
+    if constexpr (SMALLT && !FOLD) {
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         const int n = 64 * ch + lane;

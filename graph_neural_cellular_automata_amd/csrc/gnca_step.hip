@@ -1401,8 +1401,8 @@ static const Variant kVariants[] = {
     GNCA_SVF(24, 36, 4, 4, 8),   // + the fold variant (large-batch rollouts: one K1 launch per step)
     GNCA_SV(36, 24, 4, 4, 8),
     GNCA_SV(24, 24, 4, 4, 8),
-    GNCA_SV(8, 24, 4, 4, 8),
-    GNCA_SV(8, 24, 1, 4, 0),     // classic NCA (no gather; RX 4 keeps the staging rows quad-aligned)
+    GNCA_SVF(8, 24, 4, 4, 8),
+    GNCA_SVF(8, 24, 1, 4, 0),    // classic NCA (no gather; RX 4 keeps the staging rows quad-aligned)
     GNCA_SV(8, 20, 4, 4, 8),
     GNCA_SV(8, 20, 1, 4, 0),
     // 32 channels (BASELINE config 5: 128^2, r = 5, K = 16): 16x16 tiles, channel planes staged
@@ -1607,13 +1607,16 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // the fold: a fold-capable K1 on the compact field, thresholds that allow the alive hand-over
   // (0 <= alpha_thr <= graph_alpha_thr), 32-bit packed-field offsets; the second set of
   // the compact field (each field + 256 B: the finalizer's quad reads may touch one float past it)
-  P->fold_ok = P->compact_ok && P->var->fold_fn != nullptr && P->graph_on && P->k == P->var->KU &&
+  // (the update field is compact for large batches and dense NCHW for small ones)
+  P->fold_ok = P->var->fold_fn != nullptr && !msg_only && !attn_on &&
+               (P->graph_on ? P->k == P->var->KU : P->var->KU == 0) &&
                d->alpha_thr >= 0.f && d->graph_alpha_thr >= d->alpha_thr && n < (size_t)1 << 31;
+  const bool fc = P->fold_ok && P->compact_ok;
   P->off_dx2 = carve(P->fold_ok ? n * 4 + 256 : 0);
   P->off_stats2 = carve(P->fold_ok ? (size_t)P->total_tiles * P->ppt * 2 * sizeof(double) : 0);
-  P->off_rmask2 = carve(P->fold_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint64_t) : 0);
-  P->off_rpre2 = carve(P->fold_ok ? (size_t)P->total_tiles * P->TH * sizeof(uint32_t) : 0);
-  P->off_dxa2 = carve(P->fold_ok ? (size_t)d->B * d->H * d->W * sizeof(float) : 0);
+  P->off_rmask2 = carve(fc ? (size_t)P->total_tiles * P->TH * sizeof(uint64_t) : 0);
+  P->off_rpre2 = carve(fc ? (size_t)P->total_tiles * P->TH * sizeof(uint32_t) : 0);
+  P->off_dxa2 = carve(fc ? (size_t)d->B * d->H * d->W * sizeof(float) : 0);
   P->ws_bytes = o;
   if (P->need_k0) {
     const size_t k0 = ((size_t)d->C * d->H + d->C + d->d_model + P->k) * sizeof(double);
@@ -1891,15 +1894,17 @@ static int fold_k1(const gnca_step_desc* d, const gnca_weights* w, const Plan& P
   K1Args k1;
   fill_k1(k1, d, w, P, xp, cur.dx, nullptr, nullptr, wsb);
   k1.stats = cur.stats;
-  k1.rmask = cur.rmask;
-  k1.rpre = cur.rpre;
-  k1.dxa = cur.dxa;
+  if (P.compact_ok) {   // else the dense NCHW field (small batches), dead cells' zeros included
+    k1.rmask = cur.rmask;
+    k1.rpre = cur.rpre;
+    k1.dxa = cur.dxa;
+    k1.rmaskp = prev.rmask;
+    k1.rprep = prev.rpre;
+    k1.dxap = prev.dxa;
+  }
   k1.xp = xp;
   k1.xo = xo;
   k1.dxp = prev.dx;
-  k1.rmaskp = prev.rmask;
-  k1.rprep = prev.rpre;
-  k1.dxap = prev.dxa;
   k1.statsp = prev.stats;
   k1.use_gn = (d->flags & GNCA_USE_GROUPNORM) ? 1 : 0;
   k1.gamma = w->gn_weight;

@@ -429,25 +429,30 @@ def test_masked_step_many_tiles_per_workgroup(dev):
 
 
 def test_subbatch_rollout_and_pieces_bitwise(dev):
-    """A large-batch rollout that does not fold (the classic step) runs as 2 sub-batches on two
-    streams (one sub-batch's K2 beside the other's K1): bitwise the states of repeated single steps;
-    and a rollout issued in pieces with the alive masks handed over through the workspace
-    (gnca_rollout_ex_f32 ALIVE_OUT / ALIVE_IN) is bitwise the one-call rollout."""
+    """A large-batch rollout of a K1 without a fold variant (the 40^2 trainer canvas's 8x20 tiles)
+    runs as 2 sub-batches on two streams (one sub-batch's K2 beside the other's K1): bitwise the
+    states of repeated single steps; and a rollout issued in pieces with the alive masks handed over
+    through the workspace (gnca_rollout_ex_f32 ALIVE_OUT / ALIVE_IN) is bitwise the one-call
+    rollout."""
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
     m = _trained_like(dev, seed=9)
-    B, steps = 384, 5
-    x = _state(B, 16, 72, 72, dev, seed=29)
-    offs = [[] for _ in range(steps)]
+    B, steps, H = 384, 5, 40
+    x = _state(B, 16, H, H, dev, seed=29)
+    random.seed(19)
+    offs = [random.sample(m.graph.offsets, 8) for _ in range(steps)]
     w, keep = S.make_weights(dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
                                   b1=m.update_net[0].bias, w2=m.update_net[2].weight,
-                                  gn_weight=m.norm.weight, gn_bias=m.norm.bias))
+                                  gn_weight=m.norm.weight, gn_bias=m.norm.bias,
+                                  **m.graph.weight_tensors()))
 
     def desc(t):
-        return S.make_desc(B=B, C=16, H=72, W=72, hidden=128, d_model=16, offsets=[],
-                           flags=L.USE_GROUPNORM, update_gain=0.05, alpha_thr=0.12, message_gain=0.25,
-                           fire_rate=0.5, fire_mode=L.FIRE_HASH, rng_seed=3, rng_step=t, sample_base=7)
+        return S.make_desc(B=B, C=16, H=H, W=H, hidden=128, d_model=16, offsets=offs[t],
+                           flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                           update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                           fire_mode=L.FIRE_HASH, rng_seed=3, rng_step=t, sample_base=7)
 
+    assert S.k1_variant(desc(0))[0] == "gnca_k1_split<8,20,4,4,8>"
     assert S.rollout_subs(desc(0)) == 2 and not S.rollout_fold(desc(0))
     r = S.rollout(desc(0), w, x.contiguous(), steps, offs)
     cur = x
@@ -460,7 +465,8 @@ def test_subbatch_rollout_and_pieces_bitwise(dev):
     a, b2, scratch = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
     st = torch.cuda.current_stream().cuda_stream
     for (s0, n, src, dst, fl) in ((0, 2, x, a, L.ROLLOUT_ALIVE_OUT), (2, 3, a, b2, L.ROLLOUT_ALIVE_IN)):
-        arr = None
+        flat = [v for o in offs[s0:s0 + n] for p in o for v in p]
+        arr = (ctypes.c_int8 * len(flat))(*flat)
         L.check(lib.gnca_rollout_ex_f32(ctypes.byref(desc(s0)), ctypes.byref(w), n, arr, src.data_ptr(),
                                         dst.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(), fl, st),
                 "gnca_rollout_ex_f32")
@@ -483,30 +489,35 @@ def test_make_weights_cache_rejects_non_contiguous_at_cached_address(dev):
         S.make_weights({"w2": t.view(torch.int32)})
 
 
-def test_fold_rollout_pieces_bitwise(dev):
-    """The fold (each step's finish inside the next step's K1, one launch per step): a rollout issued
-    as a chain of pieces that hand the last step over unfinished (PENDING_OUT / PENDING_IN, piece
-    sizes 1, 1, 2, 3 and a single one-step piece chain) is bitwise the one-call rollout and the
+@pytest.mark.parametrize("B,graph", [(160, True), (8, True), (8, False), (160, False)])
+def test_fold_rollout_pieces_bitwise(dev, B, graph):
+    """The fold (each step's finish inside the next step's K1, one launch per step) on the compact
+    update field (B=160) and the dense one (B=8, BASELINE configs 2 and 3), graph and classic: a
+    rollout issued as a chain of pieces that hand the last step over unfinished (PENDING_OUT /
+    PENDING_IN; piece sizes 1, 1, 2, 3 / 4, 3 / 6, 1) is bitwise the one-call rollout and the
     repeated unfused single steps; bad flag combinations are rejected."""
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
     m = _trained_like(dev, seed=12)
-    B, steps = 160, 7
+    steps = 7
     x = _state(B, 16, 72, 72, dev, seed=31)
     random.seed(23)
-    offs = [random.sample(m.graph.offsets, 8) for _ in range(steps)]
-    w, keep = S.make_weights(dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
-                                  b1=m.update_net[0].bias, w2=m.update_net[2].weight,
-                                  gn_weight=m.norm.weight, gn_bias=m.norm.bias,
-                                  **m.graph.weight_tensors()))
+    offs = [random.sample(m.graph.offsets, 8) if graph else [] for _ in range(steps)]
+    tensors = dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight,
+                   b1=m.update_net[0].bias, w2=m.update_net[2].weight,
+                   gn_weight=m.norm.weight, gn_bias=m.norm.bias)
+    if graph:
+        tensors.update(m.graph.weight_tensors())
+    w, keep = S.make_weights(tensors)
+    flags = L.USE_GROUPNORM | ((L.GRAPH | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE) if graph else 0)
 
     def desc(t):
-        return S.make_desc(B=B, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[t],
-                           flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+        return S.make_desc(B=B, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[t], flags=flags,
                            update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
                            fire_mode=L.FIRE_HASH, rng_seed=11, rng_step=t, sample_base=3)
 
     assert S.rollout_fold(desc(0)) and S.rollout_subs(desc(0)) == 1
+    assert S.rollout_compact(desc(0)) == (B > 8)
     one = S.rollout(desc(0), w, x.contiguous(), steps, offs)
     cur = x
     for t in range(steps):
@@ -523,7 +534,7 @@ def test_fold_rollout_pieces_bitwise(dev):
         for i, n in enumerate(sizes):
             fl = (L.ROLLOUT_PENDING_IN if i > 0 else 0) | (L.ROLLOUT_PENDING_OUT if i + 1 < len(sizes) else 0)
             flat = [v for o in offs[s0:s0 + n] for p in o for v in p]
-            arr = (ctypes.c_int8 * len(flat))(*flat)
+            arr = (ctypes.c_int8 * len(flat))(*flat) if flat else None
             dst = outs[i % 2]
             L.check(lib.gnca_rollout_ex_f32(ctypes.byref(desc(s0)), ctypes.byref(w), n, arr, src.data_ptr(),
                                             dst.data_ptr(), scratch.data_ptr(), ws.data_ptr(), ws.numel(), fl, st),
@@ -535,17 +546,19 @@ def test_fold_rollout_pieces_bitwise(dev):
     assert torch.equal(run([4, 3]), one)
     assert torch.equal(run([6, 1]), one)
     # PENDING with ALIVE on the same side, and PENDING on a rollout that does not fold: invalid
+    if not (graph and B > 8):
+        return
     arr = (ctypes.c_int8 * 16)(*[v for p in offs[0] for v in p])
     for fl in (L.ROLLOUT_PENDING_OUT | L.ROLLOUT_ALIVE_OUT, L.ROLLOUT_PENDING_IN | L.ROLLOUT_ALIVE_IN):
         assert lib.gnca_rollout_ex_f32(ctypes.byref(desc(0)), ctypes.byref(w), 1, arr, x.data_ptr(),
                                        scratch.data_ptr(), torch.empty_like(x).data_ptr(), ws.data_ptr(),
                                        ws.numel(), fl, st) == -1
-    d8 = S.make_desc(B=8, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[0],
+    d8 = S.make_desc(B=8, C=16, H=40, W=40, hidden=128, d_model=16, offsets=offs[0],
                      flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
                      update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
                      fire_mode=L.FIRE_HASH, rng_seed=11)
-    assert not S.rollout_fold(d8)
-    x8 = x[:8].contiguous()
+    assert not S.rollout_fold(d8)   # 40^2: the 8x20 K1 has no fold variant
+    x8 = _state(8, 16, 40, 40, dev, seed=2)
     ws8 = S.workspace(d8, dev)
     assert lib.gnca_rollout_ex_f32(ctypes.byref(d8), ctypes.byref(w), 1, arr, x8.data_ptr(),
                                    torch.empty_like(x8).data_ptr(), torch.empty_like(x8).data_ptr(), ws8.data_ptr(),
