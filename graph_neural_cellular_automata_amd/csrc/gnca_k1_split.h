@@ -157,7 +157,7 @@ __host__ __device__ constexpr int ks_pstr(int rhw) {
 }
 
 struct KSLayout {
-  int xs, sp, ab, lst, cnt, cb, pg, fk, p0, p1, pbm, w1, bias, w2, wm, wz, bml, total;   // byte offsets
+  int xs, sp, ab, lst, cnt, cb, pg, fk, p0, p1, pbm, ft, w1, bias, w2, wm, wz, bml, total;   // byte offsets
   int sp_slot, lst_slot;                                             // bytes per prepared-tile slot
 };
 
@@ -188,6 +188,7 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   L.p0 = o; o += 2 * ks_a16(RH * 8);
   L.p1 = o; o += ks_a16(RH * 8);
   L.pbm = o; o += ks_a16(2 * (RH + 2) * 8);
+  L.ft = o; o += 2 * ks_a16((RH + 2) * 3 * 16);   // per slot: the previous step's row tables of the band's source tiles
   L.w1 = o; o += 3 * 4 * 3 * 1024;       // [plane][rb][kc][lane] x 16 B
   L.bias = o; o += 4 * 32 * 16;          // [rb][row] x 16 B (k slots 0..2 = the three parts)
   L.w2 = o; o += 3 * 8 * 2 * 16 * 16;    // [plane][s][h][channel] x 16 B
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   int* fctr = cnt + 4;
   int* pdone = cnt + 5;
   int fbase = 0;
-  constexpr int NQB = (NQ + 63) / 64, NFIN = 4 * NQB;
+  constexpr int NQB = (NQ + 63) / 64;   // finalize items: 64 region quads x all 16 channels
   // the fold reads the previous step's update field either compact (large batches: rmaskp != null)
   // or dense NCHW with the dead cells' zeros (small batches)
 
@@ -420,20 +421,74 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   };
 
   // ---- the fold (FOLD): the previous step's finalize, done here instead of by a K2 pass ----
-  // The preparer's part for a tile of sample b at (i0, j0), slot s: (F0) the previous step's per-
-  // sample GroupNorm constants (K2's fixed-order sums and arithmetic: fin_*); (F1) the finalized
-  // alpha x~_3 of the region plus one ring, as two threshold-bit row masks per row (ballots; lane =
-  // column of a band RW + 8 wide, quad-aligned); (F2) the 3x3 OR-pool of the bits with the
-  // max-pool's -inf border (no neighbour across the image edge, ncagraph.py:85-92) = the region's
-  // pre-update alive masks P0 (> alpha_thr) and sender masks P1 (> graph_alpha_thr), exactly the
-  // bytes K2 would have handed over; (F3) the sender plane from P1.
+  // The preparer's part for a tile of sample b at (i0, j0), slot s.  (a) Every load it needs goes out
+  // at once: the finalized-alpha band's x_3 and dx_3 (the region plus one ring, RW + 8 columns,
+  // quad-aligned: lane = column), the previous step's row tables of the band's <= 3 source tiles per
+  // row (compact field; copied to the slot for the finalizers), and the previous step's GroupNorm
+  // partials of sample b.  (b) The per-sample GroupNorm constants (K2's fixed-order sums and
+  // arithmetic: fin_*).  (c) The finalized alpha x~_3 per band cell as two threshold-bit row masks
+  // (ballots).  (d) Their 3x3 OR-pool with the max-pool's -inf border (no neighbour across the image
+  // edge, ncagraph.py:85-92) = the region's pre-update alive masks P0 (> alpha_thr) and sender
+  // masks P1 (> graph_alpha_thr): exactly the bytes K2 would have handed over.  (e) The
+  // sender plane from P1.
+  constexpr int PBH = RH + 2, PBW = RW + 8;
+  constexpr int FTS = ks_a16(PBH * 3 * 16);   // bytes per slot of the row-table copy
+  static_assert(!FOLD || PBW <= 64, "one lane per column of the pooled band");
+  static_assert(!FOLD || RX + 4 <= TW, "the band spans at most 3 source tile columns");
   auto prep_fold = [&](int b, int i0, int j0, int s) {
     float* fks = reinterpret_cast<float*>(smem_b + L.fk + s * 192);
     uint64_t* p0s = reinterpret_cast<uint64_t*>(smem_b + L.p0 + s * ks_a16(RH * 8));
     uint64_t* p1s = reinterpret_cast<uint64_t*>(smem_b + L.p1);
     uint64_t* pbm = reinterpret_cast<uint64_t*>(smem_b + L.pbm);
+    u32x4* fts = reinterpret_cast<u32x4*>(smem_b + L.ft + s * FTS);   // [band row][k]: (m lo, m hi, pre, tile)
     uint32_t* spp = reinterpret_cast<uint32_t*>(smem_b + L.sp + s * L.sp_slot);
     const bool gn = a.use_gn != 0;
+    const bool cfield = a.rmaskp != nullptr;
+    const bool lin = lane < PBW;
+    int gcol = j0 - RX - 4 + (lin ? lane : 0);
+    gcol = gcol < 0 ? gcol + W : (gcol >= W ? gcol - W : gcol);
+    int gc0 = j0 - RX;
+    gc0 = gc0 < 0 ? gc0 + W : gc0;
+    const int tx0 = gc0 / TW;                         // the source tile column of region column 0
+    int kcol = gcol / TW - tx0;
+    kcol = kcol < 0 ? kcol + a.tiles_x : kcol;        // this lane's source tile: entry k of a row
+    const int tjS = gcol - (gcol / TW) * TW;
+    const float* xpa = a.xp + ((size_t)b * C + 3) * HW;
+    const float* dpa = cfield ? a.dxap + (size_t)b * HW : a.dxp + ((size_t)b * C + 3) * HW;
+    // (a) loads
+    float xv[PBH], dv[PBH];
+#pragma unroll
+    for (int r = 0; r < PBH; ++r) {
+      int g = i0 - RY - 1 + r;
+      g = g < 0 ? g + H : (g >= H ? g - H : g);
+      const size_t cell = (size_t)g * W + gcol;
+      xv[r] = lin ? xpa[cell] : 0.f;
+      dv[r] = lin ? dpa[cell] : 0.f;
+    }
+    constexpr int NFT = PBH * 3, NFTU = (NFT + 63) / 64;
+    uint64_t fm[NFTU];
+    uint32_t fp[NFTU], ft_[NFTU];
+#pragma unroll
+    for (int u = 0; u < NFTU; ++u) {
+      const int e = 64 * u + lane;
+      fm[u] = 0ull;
+      fp[u] = 0u;
+      ft_[u] = 0u;
+      if (cfield && e < NFT) {
+        const int pr = e / 3, k = e - (e / 3) * 3;
+        int g = i0 - RY - 1 + pr;
+        g = g < 0 ? g + H : (g >= H ? g - H : g);
+        const int tyS = g / TH, tiS = g - tyS * TH;
+        int txk = tx0 + k;
+        txk = txk >= a.tiles_x ? txk - a.tiles_x : txk;
+        txk = txk >= a.tiles_x ? txk - a.tiles_x : txk;   // tiles_x may be 1
+        const uint32_t tsrc = (uint32_t)(b * a.tps + tyS * a.tiles_x + txk);
+        fm[u] = a.rmaskp[(size_t)tsrc * TH + tiS];
+        fp[u] = a.rprep[(size_t)tsrc * TH + tiS];
+        ft_[u] = tsrc;
+      }
+    }
+    // (b) GroupNorm constants
     float mu = 0.f, rs = 1.f;
     if (gn) {
       double t1, t2;
@@ -453,54 +508,34 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       fks[34] = g3;
       fks[35] = b3;
     }
-    constexpr int PBH = RH + 2, PBW = RW + 8, RB = (PBH + 1) / 2;
-    static_assert(PBW <= 64, "one lane per column of the pooled band");
-    const bool lin = lane < PBW;
-    int gcol = j0 - RX - 4 + (lin ? lane : 0);
-    gcol = gcol < 0 ? gcol + W : (gcol >= W ? gcol - W : gcol);
-    const int txS = gcol / TW, tjS = gcol - txS * TW;
-    const bool cfield = a.rmaskp != nullptr;
-    const float* xpa = a.xp + ((size_t)b * C + 3) * HW;
-    const float* dpa = cfield ? a.dxap + (size_t)b * HW : a.dxp + ((size_t)b * C + 3) * HW;
-    const uint64_t* rmb = a.rmaskp + (size_t)b * a.tps * TH;
-#pragma unroll 1
-    for (int r0 = 0; r0 < PBH; r0 += RB) {
-      float xv[RB], dv[RB];
-      uint64_t mv[RB];
+    if (cfield) {
 #pragma unroll
-      for (int u = 0; u < RB; ++u) {
-        const int r = r0 + u;
-        int g = i0 - RY - 1 + r;
-        g = g < 0 ? g + H : (g >= H ? g - H : g);
-        const int tyS = g / TH, tiS = g - tyS * TH;
-        xv[u] = 0.f;
-        dv[u] = 0.f;
-        mv[u] = ~0ull;   // dense field: every value is used (a dead cell's is 0)
-        if (lin && r < PBH) {
-          const size_t cell = (size_t)g * W + gcol;
-          xv[u] = xpa[cell];
-          dv[u] = dpa[cell];
-          if (cfield) mv[u] = rmb[(size_t)(tyS * a.tiles_x + txS) * TH + tiS];
-        }
+      for (int u = 0; u < NFTU; ++u)
+        if (64 * u + lane < NFT)
+          fts[64 * u + lane] = u32x4{(uint32_t)fm[u], (uint32_t)(fm[u] >> 32), fp[u], ft_[u]};
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // (c) the finalized alpha's threshold bits, one ballot pair per band row
+#pragma unroll
+    for (int r = 0; r < PBH; ++r) {
+      bool live = true;   // dense field: every value is used (a dead cell's is 0)
+      if (cfield) {
+        const u32x4 e = fts[r * 3 + kcol];
+        live = (((((uint64_t)e[1] << 32) | e[0]) >> tjS) & 1ull) != 0;
       }
-#pragma unroll
-      for (int u = 0; u < RB; ++u) {
-        const int r = r0 + u;
-        if (r < PBH) {
-          const bool live = ((mv[u] >> tjS) & 1ull) != 0;
-          const float xa = fin_alpha(xv[u], live ? dv[u] : 0.f, mu, rs, g3, b3, a.gain, gn);
-          const uint64_t b0 = __ballot(lin && xa > a.alpha_thr), b1 = __ballot(lin && xa > a.graph_alpha_thr);
-          if (lane == 0) {
-            pbm[r] = b0;
-            pbm[PBH + r] = b1;
-          }
-        }
+      const float xa = fin_alpha(xv[r], live ? dv[r] : 0.f, mu, rs, g3, b3, a.gain, gn);
+      const uint64_t b0 = __ballot(lin && xa > a.alpha_thr), b1 = __ballot(lin && xa > a.graph_alpha_thr);
+      if (lane == 0) {
+        pbm[r] = b0;
+        pbm[PBH + r] = b1;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // bit j of nf / nl: band column j is not the image's first / last column (its left / right
+    // (d) bit j of nf / nl: band column j is not the image's first / last column (its left / right
     // neighbour in the band is its image neighbour, not the torus wrap)
     const uint64_t nf = __ballot(lin && gcol != 0), nl = __ballot(lin && gcol != W - 1);
     auto hz = [&](uint64_t m) { return m | ((m << 1) & nf) | ((m >> 1) & nl); };
@@ -522,6 +557,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // (e) the sender plane
     if constexpr (GRAPH) {
 #pragma unroll 1
       for (int e = lane; e < NQA; e += 64) {   // 4 sender bytes per dword (band column = region column + 4)
@@ -532,13 +568,14 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     }
   };
 
-  // The finalize of tile t's staged region (slot s: its constants and P0), into the staging buffer
-  // and, for the tile's own cells, into xo: x = x_prev + tanh(GN(dx_prev)) * gain (alpha: the
-  // updated alpha times the post-update gate P0), K2's arithmetic value for value.  Items of 64
-  // region quads x 4 channels are pulled from fctr by every wave that gets here; an item's loads
-  // (row tables, x_prev quads, the live cells' packed dx) are issued before the wait for the staging
-  // buffer to be free (every group of the current tile past its staged reads), so they overlap the
-  // other waves' last groups.
+  // The finalize of tile t's staged region (slot s: its constants, P0 and row tables), into the
+  // staging buffer and, for the tile's own cells, into xo: x = x_prev + tanh(GN(dx_prev)) * gain
+  // (alpha: the updated alpha times the post-update gate P0), K2's arithmetic value for value.
+  // Items of 64 region quads x all 16 channels are pulled from fctr by every wave that gets here; an
+  // item's loads (16 x_prev quads and the quad's packed dx of every channel: one memory round trip,
+  // the row tables come from the slot) are issued before the wait for the staging buffer to be free
+  // (every group of the current tile past its staged reads), so they overlap the other waves' last
+  // groups.
   auto finalize = [&](int t, int s, int need_prep, bool wait_xsd, int qe, int xb) {
     const int b = t / a.tps, tin = t - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
@@ -547,57 +584,62 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       __builtin_amdgcn_s_sleep(1);
     const float* fks = reinterpret_cast<const float*>(smem_b + L.fk + s * 192);
     const uint64_t* p0s = reinterpret_cast<const uint64_t*>(smem_b + L.p0 + s * ks_a16(RH * 8));
+    const u32x4* fts = reinterpret_cast<const u32x4*>(smem_b + L.ft + s * FTS);
     const float mu = fks[32], rs = fks[33], g3 = fks[34], b3 = fks[35];
     const bool gn = a.use_gn != 0;
     const float g2 = -2.f * a.gain;
     const bool cfield = a.rmaskp != nullptr;
+    int gc0 = j0 - RX;
+    gc0 = gc0 < 0 ? gc0 + W : gc0;
+    const int tx0 = gc0 / TW;
     bool waited = !wait_xsd;
 #pragma unroll 1
     for (;;) {
       const int it = (__builtin_amdgcn_readfirstlane(atomicAdd(fctr, 1)) >> 6) - fbase;
-      if (it >= NFIN) break;
-      const int blk = it >> 2, cg = it & 3;
-      const int q = 64 * blk + lane;
+      if (it >= NQB) break;
+      const int q = 64 * it + lane;
       const bool qv = q < NQ;
       const int vr = qv ? q / QW : 0, vq = qv ? q - (q / QW) * QW : 0;
       int g = i0 - RY + vr, gc = j0 - RX + 4 * vq;
       g = g < 0 ? g + H : (g >= H ? g - H : g);
       gc = gc < 0 ? gc + W : (gc >= W ? gc - W : gc);
       const size_t cell = (size_t)g * W + gc;
-      f4 xq[4];
+      f4 xq[C];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        xq[u] = *reinterpret_cast<const f4*>(a.xp + ((size_t)b * C + 4 * cg + u) * HW + cell);
-      f4 dqa = {0.f, 0.f, 0.f, 0.f};
-      float dv[4][4];
+      for (int c = 0; c < C; ++c) xq[c] = *reinterpret_cast<const f4*>(a.xp + ((size_t)b * C + c) * HW + cell);
+      float dv[C][4];
       uint32_t bits = 15u;   // dense field: every value is used (a dead cell's is 0)
       if (cfield) {
-        const int tyS = g / TH, tiS = g - tyS * TH, txS = gc / TW, tjS = gc - txS * TW;
-        const uint32_t tsrc = (uint32_t)(b * a.tps + tyS * a.tiles_x + txS);
-        const uint64_t m = a.rmaskp[(size_t)tsrc * TH + tiS];
-        const uint32_t pre = a.rprep[(size_t)tsrc * TH + tiS];
-        if (cg == 0) dqa = *reinterpret_cast<const f4*>(a.dxap + (size_t)b * HW + cell);
+        int k = gc / TW - tx0;
+        k = k < 0 ? k + a.tiles_x : k;
+        const u32x4 e = fts[(vr + 1) * 3 + k];
+        const uint64_t m = ((uint64_t)e[1] << 32) | e[0];
+        const int tjS = gc - (gc / TW) * TW;
         // the quad's live cells are consecutive in the source tile's packed field: cell k's value
         // (or, for a dead cell, the next live one's; never used) at rank r0 + (live cells before k)
         bits = (uint32_t)(m >> tjS) & 15u;
-        const uint32_t r0 = tsrc * (uint32_t)(C * NCELL) + pre + (uint32_t)__popcll(m & ((1ull << tjS) - 1ull));
+        const uint32_t r0 = e[3] * (uint32_t)(C * NCELL) + e[2] + (uint32_t)__popcll(m & ((1ull << tjS) - 1ull));
         uint32_t off[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) off[k] = r0 + (uint32_t)__popc(bits & ((1u << k) - 1u));
+        for (int kk = 0; kk < 4; ++kk) off[kk] = r0 + (uint32_t)__popc(bits & ((1u << kk) - 1u));
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int c = 4 * cg + u;
-          const float* fb = a.dxp + (size_t)c * NCELL;
+        for (int c = 0; c < C; ++c) {
+          if (c == 3) {
+            const f4 d4 = *reinterpret_cast<const f4*>(a.dxap + (size_t)b * HW + cell);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) dv[u][k] = c == 3 ? 0.f : fb[off[k]];
+            for (int kk = 0; kk < 4; ++kk) dv[c][kk] = d4[kk];
+          } else {
+            const float* fb = a.dxp + (size_t)c * NCELL;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) dv[c][kk] = fb[off[kk]];
+          }
         }
       } else {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const f4 d4 = *reinterpret_cast<const f4*>(a.dxp + ((size_t)b * C + 4 * cg + u) * HW + cell);
-          if (4 * cg + u == 3) dqa = d4;
+        for (int c = 0; c < C; ++c) {
+          const f4 d4 = *reinterpret_cast<const f4*>(a.dxp + ((size_t)b * C + c) * HW + cell);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) dv[u][k] = d4[k];
+          for (int kk = 0; kk < 4; ++kk) dv[c][kk] = d4[kk];
         }
       }
       if (!waited) {
@@ -606,21 +648,21 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         waited = true;
       }
       const bool own = vr >= RY && vr < RY + TH && vq >= RX / 4 && vq < (RX + TW) / 4;
+      const uint64_t pm = p0s[vr] >> (4 * vq + 4);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c = 4 * cg + u;
+      for (int c = 0; c < C; ++c) {
         f4 v;
         if (c == 3) {
-          const uint64_t pm = p0s[vr] >> (4 * vq + 4);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float xa = fin_alpha(xq[u][k], ((bits >> k) & 1u) ? dqa[k] : 0.f, mu, rs, g3, b3, a.gain, gn);
-            v[k] = xa * (((pm >> k) & 1ull) ? 1.f : 0.f);
+          for (int kk = 0; kk < 4; ++kk) {
+            const float xa = fin_alpha(xq[c][kk], ((bits >> kk) & 1u) ? dv[c][kk] : 0.f, mu, rs, g3, b3, a.gain, gn);
+            v[kk] = xa * (((pm >> kk) & 1ull) ? 1.f : 0.f);
           }
         } else {
           const float sc = fks[c], sh = fks[16 + c];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] = k2_update(xq[u][k], ((bits >> k) & 1u) ? dv[u][k] : 0.f, sc, sh, a.gain, g2);
+          for (int kk = 0; kk < 4; ++kk)
+            v[kk] = k2_update(xq[c][kk], ((bits >> kk) & 1u) ? dv[c][kk] : 0.f, sc, sh, a.gain, g2);
         }
         if (qv) {
           *reinterpret_cast<f4*>(xs + c * PSTR + 4 * q) = v;
@@ -628,7 +670,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         }
       }
     }
-    fbase += NFIN + NW;
+    fbase += NQB + NW;
   };
 
   // The preparer (one wave, no workgroup barrier): a tile's sender plane over the region, its keep

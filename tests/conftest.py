@@ -11,11 +11,7 @@ if ROOT not in sys.path:
 # The multi-rank GPU tests (test_gpu_multirank.py) start their ranks as forks of a forkserver that
 # is started HERE, before any test touches the GPU: on the GPU pool a process that has initialised
 # the GPU must never exec another program, and a forkserver child never execs at all.
-FORKSERVER_READY = False
-
-
 def pytest_configure(config):
-    global FORKSERVER_READY
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); runs through the C-ABI")
     if "not gpu" in (config.getoption("markexpr") or ""):
         return
@@ -27,4 +23,6 @@ def pytest_configure(config):
         return
     mp.get_context("forkserver").set_forkserver_preload([])
     fs.ensure_running()
-    FORKSERVER_READY = True
+    # an environment flag, not a module global: pytest may import this file under another module name
+    # than the tests' `from tests import conftest`
+    os.environ["GNCA_FORKSERVER_READY"] = "1"

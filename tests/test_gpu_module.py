@@ -196,7 +196,7 @@ def test_compact_rollout_equals_dense_steps(dev, graph):
 
     name, arith = S.k1_variant(desc(0))
     assert arith == "bf16x6", name
-    assert S.rollout_fold(desc(0)) == graph   # the graph rollout folds each finish into the next K1
+    assert S.rollout_fold(desc(0))   # each step's finish is folded into the next step's K1
     r = S.rollout(desc(0), w, x.contiguous(), steps, offs)
     cur = x
     for t in range(steps):

@@ -32,8 +32,8 @@ def dev():
 def _run_ranks(target, args_of_rank, timeout=100):
     import multiprocessing as mp
 
-    from tests import conftest
-    assert conftest.FORKSERVER_READY, "the forkserver must start before the GPU is initialised (conftest)"
+    assert os.environ.get("GNCA_FORKSERVER_READY") == "1", \
+        "the forkserver must start before the GPU is initialised (tests/conftest.py)"
     ctx = mp.get_context("forkserver")
     q = ctx.Queue()
     port = 29900 + (os.getpid() % 500)
