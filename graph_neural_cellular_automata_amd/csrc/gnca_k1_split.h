@@ -455,15 +455,15 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const int tjS = gcol - (gcol / TW) * TW;
     const float* xpa = a.xp + ((size_t)b * C + 3) * HW;
     const float* dpa = cfield ? a.dxap + (size_t)b * HW : a.dxp + ((size_t)b * C + 3) * HW;
-    // (a) loads
+    // (a) loads (lanes past the band read column gcol of lane 0: valid, and masked out of the ballots)
     float xv[PBH], dv[PBH];
 #pragma unroll
     for (int r = 0; r < PBH; ++r) {
       int g = i0 - RY - 1 + r;
       g = g < 0 ? g + H : (g >= H ? g - H : g);
       const size_t cell = (size_t)g * W + gcol;
-      xv[r] = lin ? xpa[cell] : 0.f;
-      dv[r] = lin ? dpa[cell] : 0.f;
+      xv[r] = xpa[cell];
+      dv[r] = dpa[cell];
     }
     constexpr int NFT = PBH * 3, NFTU = (NFT + 63) / 64;
     uint64_t fm[NFTU];
@@ -517,20 +517,24 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // (c) the finalized alpha's threshold bits, one ballot pair per band row
+    // (c) the finalized alpha's threshold bits, one ballot pair per band row, kept on lane r (selects,
+    //     no per-row branch) and stored once
+    uint64_t m0r = 0ull, m1r = 0ull;
 #pragma unroll
     for (int r = 0; r < PBH; ++r) {
       bool live = true;   // dense field: every value is used (a dead cell's is 0)
       if (cfield) {
-        const u32x4 e = fts[r * 3 + kcol];
-        live = (((((uint64_t)e[1] << 32) | e[0]) >> tjS) & 1ull) != 0;
+        const uint64_t m = *reinterpret_cast<const uint64_t*>(&fts[r * 3 + kcol]);
+        live = ((m >> tjS) & 1ull) != 0;
       }
       const float xa = fin_alpha(xv[r], live ? dv[r] : 0.f, mu, rs, g3, b3, a.gain, gn);
       const uint64_t b0 = __ballot(lin && xa > a.alpha_thr), b1 = __ballot(lin && xa > a.graph_alpha_thr);
-      if (lane == 0) {
-        pbm[r] = b0;
-        pbm[PBH + r] = b1;
-      }
+      m0r = lane == r ? b0 : m0r;
+      m1r = lane == r ? b1 : m1r;
+    }
+    if (lane < PBH) {
+      pbm[lane] = m0r;
+      pbm[PBH + lane] = m1r;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

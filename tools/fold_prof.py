@@ -1,0 +1,77 @@
+"""Phase timers of the rollout's K1 launches (measurement tool, not a test): the plain K1 (a one-step
+rollout) and the fold K1 (the last K1 of a three-step rollout) of the bench workload, from a
+-DGNCA_PROFILE build (s_memtime cycles per phase, summed over each workgroup's tiles; waves 0 and 3).
+
+  python tools/fold_prof.py build     # in the build container (hipcc)
+  python tools/fold_prof.py run       # on the GPU box
+"""
+import ctypes
+import os
+import random
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "build_ablate")
+LIB = os.path.join(OUT, "lib_foldprof.so")
+NAMES = ["stage(dma|finalize)", "prologue_wait", "gather+perc", "preparer", "group_mfma+epi", "partial_bins",
+         "barrier_after_groups", "loop_top"]
+
+
+def build():
+    os.makedirs(OUT, exist_ok=True)
+    src = [os.path.join(ROOT, "graph_neural_cellular_automata_amd", "csrc", f) for f in
+           ("gnca_step.hip", "gnca_bwd.hip", "gnca_aux.hip")]
+    objs = []
+    for s in src:
+        o = os.path.join(OUT, os.path.basename(s) + ".prof.o")
+        extra = ["-fno-slp-vectorize", "-DGNCA_PROFILE"] if s.endswith("gnca_step.hip") else []
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
+                        *extra, f"-I{ROOT}/include", s, "-o", o], check=True, stderr=subprocess.DEVNULL)
+        objs.append(o)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB], check=True)
+
+
+def run():
+    os.environ["GNCA_LIB_PATH"] = LIB
+    import numpy as np
+    import torch
+    import bench
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    lib = L.load(LIB)
+    lib.gnca_prof_dump.restype = ctypes.c_int
+    dev = torch.device("cuda:0")
+    wl = bench.WORKLOADS[os.environ.get("FOLDPROF_CONFIG", "headline")]
+    B, H = wl["B"], wl["H"]
+    w, keep = bench.weight_struct(bench.load_weights(dev, wl), wl)
+    g = torch.Generator(device=dev).manual_seed(1234)
+    x = torch.rand(B, wl["C"], H, H, device=dev, generator=g)
+    x[:, 4:] = torch.randn(B, wl["C"] - 4, H, H, device=dev, generator=g)
+    from graph_neural_cellular_automata_amd.modules.graph_augmentation import GraphAugmentation
+    table = GraphAugmentation._build_offsets(wl["R"]) if wl["graph"] else []
+    rr = random.Random(0)
+    for steps in (1, 3, 1, 3):
+        offs = [rr.sample(table, wl["K"]) if wl["graph"] else [] for _ in range(steps)]
+        d = bench.make_desc(wl, B, H, H, offs[0], 0)
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        S.rollout(d, w, x, steps, offs)
+        e1.record()
+        torch.cuda.synchronize()
+        buf = (ctypes.c_ulonglong * (1024 * 16))()
+        assert lib.gnca_prof_dump(buf) == 0
+        full = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16).astype(np.float64)
+        kind = "plain K1 (1-step rollout)" if steps == 1 else "fold K1 (last K1 of a 3-step rollout)"
+        print(f"== {kind}: rollout {e0.elapsed_time(e1):.3f} ms (profile build), fold={S.rollout_fold(d)}")
+        for title, a in (("wave 0 (SIMD 0)", full[:, :8]), ("wave 3 (preparer)", full[:, 8:])):
+            a = a[a.sum(1) > 0]
+            tot = a.sum(1).mean()
+            print(f" {title}: mean cycles per workgroup {tot:.0f} over {len(a)} WGs")
+            for i, nm in enumerate(NAMES):
+                print(f"  {nm:22s} {a[:, i].mean():12.0f} cycles  {100 * a[:, i].mean() / tot:5.1f} %")
+
+
+if __name__ == "__main__":
+    build() if sys.argv[1] == "build" else run()
