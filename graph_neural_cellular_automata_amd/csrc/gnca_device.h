@@ -192,6 +192,25 @@ __device__ __forceinline__ void wave_sum2(const double* p, int n, double* s0, do
   *s1 = __shfl(y, 0);
 }
 
+// wave_sum2 for n <= 256 pairs with the pairs already in registers (lane l holds pairs l + 64 j,
+// j = 0..3, zeros past n): the same additions in the same order, so the same bits.  Lets a caller
+// issue the partials' loads together with its other loads.
+__device__ __forceinline__ void wave_sum2_regs(const double (&a)[4], const double (&b)[4], double* s0,
+                                               double* s1) {
+  double x = 0.0, y = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    x += a[j];
+    y += b[j];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    x += __shfl_xor(x, off);
+    y += __shfl_xor(y, off);
+  }
+  *s0 = __shfl(x, 0);
+  *s1 = __shfl(y, 0);
+}
+
 // Where the forward keeps its intermediates in the step workspace (gnca_step.hip:make_plan);
 // the backward recomputes them there.
 struct FwdLayout {

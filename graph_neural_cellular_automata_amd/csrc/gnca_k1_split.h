@@ -325,7 +325,9 @@ __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst)
 #define GNCA_DMA_WAVES 1   // A/B builds: waves (the first failing pulls) sharing the next tile's DMA (3: K1 0.4015-0.4044 vs 0.4008-0.4026 ms with 1)
 #endif
 
-template <int TH, int TW, int RY, int RX, int KU, bool FOLD = false>
+// FOLD: 0 = the plain K1; 1 / 2 = the fold variant (this launch also finishes the previous step,
+// below) on the previous step's dense / compact update field
+template <int TH, int TW, int RY, int RX, int KU, int FOLD = 0>
 __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_b[];
   constexpr int C = 16, HD = 128, NT = GNCA_K1_SPLIT_NT, NW = NT / 64;
@@ -360,8 +362,9 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   int* pdone = cnt + 5;
   int fbase = 0;
   constexpr int NQB = (NQ + 63) / 64;   // finalize items: 64 region quads x all 16 channels
-  // the fold reads the previous step's update field either compact (large batches: rmaskp != null)
-  // or dense NCHW with the dead cells' zeros (small batches)
+  // the fold reads the previous step's update field either compact (large batches) or dense NCHW
+  // with the dead cells' zeros (small batches)
+  constexpr bool CF = FOLD == 2;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   wg_stamp(a.stamps, 0);
@@ -443,7 +446,6 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     u32x4* fts = reinterpret_cast<u32x4*>(smem_b + L.ft + s * FTS);   // [band row][k]: (m lo, m hi, pre, tile)
     uint32_t* spp = reinterpret_cast<uint32_t*>(smem_b + L.sp + s * L.sp_slot);
     const bool gn = a.use_gn != 0;
-    const bool cfield = a.rmaskp != nullptr;
     const bool lin = lane < PBW;
     int gcol = j0 - RX - 4 + (lin ? lane : 0);
     gcol = gcol < 0 ? gcol + W : (gcol >= W ? gcol - W : gcol);
@@ -454,27 +456,31 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     kcol = kcol < 0 ? kcol + a.tiles_x : kcol;        // this lane's source tile: entry k of a row
     const int tjS = gcol - (gcol / TW) * TW;
     const float* xpa = a.xp + ((size_t)b * C + 3) * HW;
-    const float* dpa = cfield ? a.dxap + (size_t)b * HW : a.dxp + ((size_t)b * C + 3) * HW;
-    // (a) loads (lanes past the band read column gcol of lane 0: valid, and masked out of the ballots)
+    const float* dpa = CF ? a.dxap + (size_t)b * HW : a.dxp + ((size_t)b * C + 3) * HW;
+    // (a) every global load of the preparation, issued together (lanes past the band read column
+    //     gcol of lane 0: valid, and masked out of the ballots)
+    // (the row offset walks in a VGPR: kept per lane, the 2 x PBH row addresses would be scalar
+    //  pairs and spill)
     float xv[PBH], dv[PBH];
+    {
+      int g0 = i0 - RY - 1;
+      g0 = g0 < 0 ? g0 + H : g0;
+      uint32_t off = (uint32_t)(g0 * W + gcol);
 #pragma unroll
-    for (int r = 0; r < PBH; ++r) {
-      int g = i0 - RY - 1 + r;
-      g = g < 0 ? g + H : (g >= H ? g - H : g);
-      const size_t cell = (size_t)g * W + gcol;
-      xv[r] = xpa[cell];
-      dv[r] = dpa[cell];
+      for (int r = 0; r < PBH; ++r) {
+        xv[r] = xpa[off];
+        dv[r] = dpa[off];
+        off += (uint32_t)W;
+        off = off >= (uint32_t)HW ? off - (uint32_t)HW : off;   // the torus wrap of the next row
+      }
     }
     constexpr int NFT = PBH * 3, NFTU = (NFT + 63) / 64;
     uint64_t fm[NFTU];
     uint32_t fp[NFTU], ft_[NFTU];
+    if constexpr (CF) {
 #pragma unroll
-    for (int u = 0; u < NFTU; ++u) {
-      const int e = 64 * u + lane;
-      fm[u] = 0ull;
-      fp[u] = 0u;
-      ft_[u] = 0u;
-      if (cfield && e < NFT) {
+      for (int u = 0; u < NFTU; ++u) {
+        const int e = min(64 * u + lane, NFT - 1);
         const int pr = e / 3, k = e - (e / 3) * 3;
         int g = i0 - RY - 1 + pr;
         g = g < 0 ? g + H : (g >= H ? g - H : g);
@@ -488,17 +494,31 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         ft_[u] = tsrc;
       }
     }
+    // the previous step's GroupNorm partials of sample b (nst <= 256, host-checked: wave_sum2's
+    // single pass) and the affine parameters
+    const double* stp = a.statsp + (size_t)b * a.nst * 2;
+    double sa[4], sb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = lane + 64 * j;
+      const int tc = min(t, a.nst - 1);
+      const double pa = stp[2 * tc], pb = stp[2 * tc + 1];
+      sa[j] = t < a.nst ? pa : 0.0;
+      sb[j] = t < a.nst ? pb : 0.0;
+    }
+    const int lc = lane < C ? lane : 0;
+    const float gam_l = a.gamma ? a.gamma[lc] : 1.f, bet_l = a.beta ? a.beta[lc] : 0.f;
     // (b) GroupNorm constants
     float mu = 0.f, rs = 1.f;
     if (gn) {
       double t1, t2;
-      wave_sum2(a.statsp + (size_t)b * a.nst * 2, a.nst, &t1, &t2);
+      wave_sum2_regs(sa, sb, &t1, &t2);
       fin_mu_rs(t1, t2, (double)C * (double)HW, a.eps, &mu, &rs);
     }
-    const float g3 = gn ? a.gamma[3] : 1.f, b3 = gn ? a.beta[3] : 0.f;
+    const float g3 = gn ? __shfl(gam_l, 3) : 1.f, b3 = gn ? __shfl(bet_l, 3) : 0.f;
     if (lane < C) {
       float sc, sh;
-      fin_consts(gn ? a.gamma[lane] : 1.f, gn ? a.beta[lane] : 0.f, mu, rs, gn, &sc, &sh);
+      fin_consts(gn ? gam_l : 1.f, gn ? bet_l : 0.f, mu, rs, gn, &sc, &sh);
       fks[lane] = sc;
       fks[16 + lane] = sh;
     }
@@ -508,33 +528,29 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       fks[34] = g3;
       fks[35] = b3;
     }
-    if (cfield) {
+    if constexpr (CF) {
 #pragma unroll
       for (int u = 0; u < NFTU; ++u)
         if (64 * u + lane < NFT)
           fts[64 * u + lane] = u32x4{(uint32_t)fm[u], (uint32_t)(fm[u] >> 32), fp[u], ft_[u]};
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // (c) the finalized alpha's threshold bits, one ballot pair per band row, kept on lane r (selects,
-    //     no per-row branch) and stored once
-    uint64_t m0r = 0ull, m1r = 0ull;
+    // (c) the finalized alpha's threshold bits, one ballot pair per band row
 #pragma unroll
     for (int r = 0; r < PBH; ++r) {
       bool live = true;   // dense field: every value is used (a dead cell's is 0)
-      if (cfield) {
+      if constexpr (CF) {
         const uint64_t m = *reinterpret_cast<const uint64_t*>(&fts[r * 3 + kcol]);
         live = ((m >> tjS) & 1ull) != 0;
       }
       const float xa = fin_alpha(xv[r], live ? dv[r] : 0.f, mu, rs, g3, b3, a.gain, gn);
       const uint64_t b0 = __ballot(lin && xa > a.alpha_thr), b1 = __ballot(lin && xa > a.graph_alpha_thr);
-      m0r = lane == r ? b0 : m0r;
-      m1r = lane == r ? b1 : m1r;
-    }
-    if (lane < PBH) {
-      pbm[lane] = m0r;
-      pbm[PBH + lane] = m1r;
+      if (lane == 0) {   // stored right away: no scalar pair stays live past its row
+        pbm[r] = b0;
+        pbm[PBH + r] = b1;
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -592,7 +608,6 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const float mu = fks[32], rs = fks[33], g3 = fks[34], b3 = fks[35];
     const bool gn = a.use_gn != 0;
     const float g2 = -2.f * a.gain;
-    const bool cfield = a.rmaskp != nullptr;
     int gc0 = j0 - RX;
     gc0 = gc0 < 0 ? gc0 + W : gc0;
     const int tx0 = gc0 / TW;
@@ -613,7 +628,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       for (int c = 0; c < C; ++c) xq[c] = *reinterpret_cast<const f4*>(a.xp + ((size_t)b * C + c) * HW + cell);
       float dv[C][4];
       uint32_t bits = 15u;   // dense field: every value is used (a dead cell's is 0)
-      if (cfield) {
+      if constexpr (CF) {
         int k = gc / TW - tx0;
         k = k < 0 ? k + a.tiles_x : k;
         const u32x4 e = fts[(vr + 1) * 3 + k];

@@ -1381,28 +1381,32 @@ struct Variant {
   int NT;                            // threads per workgroup
   int split;                         // 1: gnca_k1_split, 2: gnca_k1_split32 (bf16 MFMA on exact 3-way splits)
   int lds_split;                     // its LDS bytes (compile-time layout)
-  const void* fold_fn;               // the same K1 that also finishes the previous step (rollouts), or null
+  const void* fold_fn[2];            // the same K1 that also finishes the previous step (rollouts) on the
+                                     // [dense, compact] update field, or null
 };
 
-#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0, nullptr}
+#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0, {nullptr, nullptr}}
 #define GNCA_SV(th, tw, ry, rx, ku) \
   {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
-   ks_layout<th, tw, ry, rx>().total, nullptr}
-#define GNCA_SVF(th, tw, ry, rx, ku) \
+   ks_layout<th, tw, ry, rx>().total, {nullptr, nullptr}}
+// fold variants: the large-batch tile (dense: nullptr, it is only planned with the compact field) and
+// the small-batch ones (both layouts)
+#define GNCA_SVF(th, tw, ry, rx, ku, dense) \
   {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
-   ks_layout<th, tw, ry, rx>().total, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku, true>)}
+   ks_layout<th, tw, ry, rx>().total, {dense, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku, 2>)}}
 #define GNCA_S32V(th, tw, ry, rx, ku) \
   {32, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split32<th, tw, ry, rx, ku>), 512, 2, \
-   ks32_layout<th, tw, ry, rx>().total, nullptr}
+   ks32_layout<th, tw, ry, rx>().total, {nullptr, nullptr}}
 static const Variant kVariants[] = {
     // 16 channels, hidden 128, bf16 MFMA on exact 3-way splits (gnca_k1_split.h), compile-time
     // geometry: list order is the large-batch preference (24x36: the largest tiles whose halo fits
     // LDS, 1.6x halo re-read); 8x24 / 8x20 serve small batches and the trainer's 40^2 canvas
-    GNCA_SVF(24, 36, 4, 4, 8),   // + the fold variant (large-batch rollouts: one K1 launch per step)
+    GNCA_SVF(24, 36, 4, 4, 8, nullptr),   // + the fold variant (large-batch rollouts: one K1 launch per step)
     GNCA_SV(36, 24, 4, 4, 8),
     GNCA_SV(24, 24, 4, 4, 8),
-    GNCA_SVF(8, 24, 4, 4, 8),
-    GNCA_SVF(8, 24, 1, 4, 0),    // classic NCA (no gather; RX 4 keeps the staging rows quad-aligned)
+    GNCA_SVF(8, 24, 4, 4, 8, reinterpret_cast<const void*>(&gnca_k1_split<8, 24, 4, 4, 8, 1>)),
+    GNCA_SVF(8, 24, 1, 4, 0, reinterpret_cast<const void*>(&gnca_k1_split<8, 24, 1, 4, 0, 1>)),   // classic NCA
+                                 // (no gather; RX 4 keeps the staging rows quad-aligned)
     GNCA_SV(8, 20, 4, 4, 8),
     GNCA_SV(8, 20, 1, 4, 0),
     // 32 channels (BASELINE config 5: 128^2, r = 5, K = 16): 16x16 tiles, channel planes staged
@@ -1608,9 +1612,11 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // (0 <= alpha_thr <= graph_alpha_thr), 32-bit packed-field offsets; the second set of
   // the compact field (each field + 256 B: the finalizer's quad reads may touch one float past it)
   // (the update field is compact for large batches and dense NCHW for small ones)
-  P->fold_ok = P->var->fold_fn != nullptr && !msg_only && !attn_on &&
+  // (the preparer sums a sample's partials in one wave pass: tps * waves <= 256)
+  P->fold_ok = P->var->fold_fn[P->compact_ok ? 1 : 0] != nullptr && !msg_only && !attn_on &&
                (P->graph_on ? P->k == P->var->KU : P->var->KU == 0) &&
-               d->alpha_thr >= 0.f && d->graph_alpha_thr >= d->alpha_thr && n < (size_t)1 << 31;
+               d->alpha_thr >= 0.f && d->graph_alpha_thr >= d->alpha_thr && n < (size_t)1 << 31 &&
+               P->tps * P->ppt <= 256;
   const bool fc = P->fold_ok && P->compact_ok;
   P->off_dx2 = carve(P->fold_ok ? n * 4 + 256 : 0);
   P->off_stats2 = carve(P->fold_ok ? (size_t)P->total_tiles * P->ppt * 2 * sizeof(double) : 0);
@@ -1914,12 +1920,13 @@ static int fold_k1(const gnca_step_desc* d, const gnca_weights* w, const Plan& P
   k1.nst = P.tps * P.ppt;
   k1.wimg = wimg;
   k1.stamps = stamps;
-  const int occ = occupancy(P.var->fold_fn, P.lds1, P.var->NT);
+  const void* fn = P.var->fold_fn[P.compact_ok ? 1 : 0];
+  const int occ = occupancy(fn, P.lds1, P.var->NT);
   long grid = std::min<long>((long)device_cus() * occ, P.total_tiles);
   if (grid < 1) grid = 1;
   if (stamps && grid > stamp_cap) return GNCA_ERR_INVALID;
   void* args[] = {&k1};
-  const hipError_t e = hipLaunchKernel(P.var->fold_fn, dim3((unsigned)grid), dim3(P.var->NT), args, P.lds1, st);
+  const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(P.var->NT), args, P.lds1, st);
   if (e != hipSuccess) {
     g_last_hip = (int)e;
     return GNCA_ERR_HIP;
