@@ -361,13 +361,15 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   int* fctr = cnt + 4;
   int* pdone = cnt + 5;
   int fbase = 0;
-  constexpr int NQB = (NQ + 63) / 64;   // finalize items: 64 region quads x all 16 channels
+  constexpr int NQB = (NQ + 63) / 64;
+  constexpr int FCH = 8, NFIT = NQB * (C / FCH);   // finalize items: 64 region quads x 8 channels
   // the fold reads the previous step's update field either compact (large batches) or dense NCHW
   // with the dead cells' zeros (small batches)
   constexpr bool CF = FOLD == 2;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   wg_stamp(a.stamps, 0);
+  FPROF_DECL
   if constexpr (FOLD) {   // the fold's counters are used before the prologue's barrier
     if (tid == 0) { *fctr = 0; *pdone = 0; }
     __syncthreads();
@@ -457,6 +459,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const int tjS = gcol - (gcol / TW) * TW;
     const float* xpa = a.xp + ((size_t)b * C + 3) * HW;
     const float* dpa = CF ? a.dxap + (size_t)b * HW : a.dxp + ((size_t)b * C + 3) * HW;
+    FPROF_START();
     // (a) every global load of the preparation, issued together (lanes past the band read column
     //     gcol of lane 0: valid, and masked out of the ballots)
     // (the row offset walks in a VGPR: kept per lane, the 2 x PBH row addresses would be scalar
@@ -508,6 +511,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     }
     const int lc = lane < C ? lane : 0;
     const float gam_l = a.gamma ? a.gamma[lc] : 1.f, bet_l = a.beta ? a.beta[lc] : 0.f;
+    FPROF_MARK(4);
     // (b) GroupNorm constants
     float mu = 0.f, rs = 1.f;
     if (gn) {
@@ -537,14 +541,18 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    FPROF_MARK(5);
     // (c) the finalized alpha's threshold bits, one ballot pair per band row
+    // (the compact field's live bits of this lane's column, all rows read from the slot first)
+    uint32_t lv[PBH];
 #pragma unroll
     for (int r = 0; r < PBH; ++r) {
-      bool live = true;   // dense field: every value is used (a dead cell's is 0)
-      if constexpr (CF) {
-        const uint64_t m = *reinterpret_cast<const uint64_t*>(&fts[r * 3 + kcol]);
-        live = ((m >> tjS) & 1ull) != 0;
-      }
+      lv[r] = 1u;   // dense field: every value is used (a dead cell's is 0)
+      if constexpr (CF) lv[r] = (uint32_t)(*reinterpret_cast<const uint64_t*>(&fts[r * 3 + kcol]) >> tjS) & 1u;
+    }
+#pragma unroll
+    for (int r = 0; r < PBH; ++r) {
+      const bool live = lv[r] != 0;
       const float xa = fin_alpha(xv[r], live ? dv[r] : 0.f, mu, rs, g3, b3, a.gain, gn);
       const uint64_t b0 = __ballot(lin && xa > a.alpha_thr), b1 = __ballot(lin && xa > a.graph_alpha_thr);
       if (lane == 0) {   // stored right away: no scalar pair stays live past its row
@@ -555,6 +563,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    FPROF_MARK(6);
     // (d) bit j of nf / nl: band column j is not the image's first / last column (its left / right
     // neighbour in the band is its image neighbour, not the torus wrap)
     const uint64_t nf = __ballot(lin && gcol != 0), nl = __ballot(lin && gcol != W - 1);
@@ -574,9 +583,13 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       p0s[lane] = q0;
       p1s[lane] = q1;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // what the finalizers read (the constants, P0, the row tables) is complete: they may start now,
+    // beside the rest of this preparation (the sender plane, the keep mask, the live list)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    FPROF_MARK(7);
     // (e) the sender plane
     if constexpr (GRAPH) {
 #pragma unroll 1
@@ -586,6 +599,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         spp[e] = a2a ? ((bits & 1u) | ((bits & 2u) << 7) | ((bits & 4u) << 14) | ((bits & 8u) << 21)) : 0x01010101u;
       }
     }
+    FPROF_MARK(8);
   };
 
   // The finalize of tile t's staged region (slot s: its constants, P0 and row tables), into the
@@ -600,8 +614,10 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const int b = t / a.tps, tin = t - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
+    FPROF_START();
     while (__hip_atomic_load(pdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need_prep)
       __builtin_amdgcn_s_sleep(1);
+    FPROF_MARK(0);
     const float* fks = reinterpret_cast<const float*>(smem_b + L.fk + s * 192);
     const uint64_t* p0s = reinterpret_cast<const uint64_t*>(smem_b + L.p0 + s * ks_a16(RH * 8));
     const u32x4* fts = reinterpret_cast<const u32x4*>(smem_b + L.ft + s * FTS);
@@ -615,18 +631,19 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
 #pragma unroll 1
     for (;;) {
       const int it = (__builtin_amdgcn_readfirstlane(atomicAdd(fctr, 1)) >> 6) - fbase;
-      if (it >= NQB) break;
-      const int q = 64 * it + lane;
+      if (it >= NFIT) break;
+      const int c0 = FCH * (it % (C / FCH));
+      const int q = 64 * (it / (C / FCH)) + lane;
       const bool qv = q < NQ;
       const int vr = qv ? q / QW : 0, vq = qv ? q - (q / QW) * QW : 0;
       int g = i0 - RY + vr, gc = j0 - RX + 4 * vq;
       g = g < 0 ? g + H : (g >= H ? g - H : g);
       gc = gc < 0 ? gc + W : (gc >= W ? gc - W : gc);
       const size_t cell = (size_t)g * W + gc;
-      f4 xq[C];
+      f4 xq[FCH];
 #pragma unroll
-      for (int c = 0; c < C; ++c) xq[c] = *reinterpret_cast<const f4*>(a.xp + ((size_t)b * C + c) * HW + cell);
-      float dv[C][4];
+      for (int u = 0; u < FCH; ++u) xq[u] = *reinterpret_cast<const f4*>(a.xp + ((size_t)b * C + c0 + u) * HW + cell);
+      float dv[FCH][4];
       uint32_t bits = 15u;   // dense field: every value is used (a dead cell's is 0)
       if constexpr (CF) {
         int k = gc / TW - tx0;
@@ -642,23 +659,24 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) off[kk] = r0 + (uint32_t)__popc(bits & ((1u << kk) - 1u));
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
+        for (int u = 0; u < FCH; ++u) {
+          const int c = c0 + u;
           if (c == 3) {
             const f4 d4 = *reinterpret_cast<const f4*>(a.dxap + (size_t)b * HW + cell);
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) dv[c][kk] = d4[kk];
+            for (int kk = 0; kk < 4; ++kk) dv[u][kk] = d4[kk];
           } else {
             const float* fb = a.dxp + (size_t)c * NCELL;
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) dv[c][kk] = fb[off[kk]];
+            for (int kk = 0; kk < 4; ++kk) dv[u][kk] = fb[off[kk]];
           }
         }
       } else {
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const f4 d4 = *reinterpret_cast<const f4*>(a.dxp + ((size_t)b * C + c) * HW + cell);
+        for (int u = 0; u < FCH; ++u) {
+          const f4 d4 = *reinterpret_cast<const f4*>(a.dxp + ((size_t)b * C + c0 + u) * HW + cell);
 #pragma unroll
-          for (int kk = 0; kk < 4; ++kk) dv[c][kk] = d4[kk];
+          for (int kk = 0; kk < 4; ++kk) dv[u][kk] = d4[kk];
         }
       }
       if (!waited) {
@@ -666,30 +684,34 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
           __builtin_amdgcn_s_sleep(1);
         waited = true;
       }
+      FPROF_MARK(1);
+      FPROF_COUNT(3);
       const bool own = vr >= RY && vr < RY + TH && vq >= RX / 4 && vq < (RX + TW) / 4;
       const uint64_t pm = p0s[vr] >> (4 * vq + 4);
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
+      for (int u = 0; u < FCH; ++u) {
+        const int c = c0 + u;
         f4 v;
         if (c == 3) {
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
-            const float xa = fin_alpha(xq[c][kk], ((bits >> kk) & 1u) ? dv[c][kk] : 0.f, mu, rs, g3, b3, a.gain, gn);
+            const float xa = fin_alpha(xq[u][kk], ((bits >> kk) & 1u) ? dv[u][kk] : 0.f, mu, rs, g3, b3, a.gain, gn);
             v[kk] = xa * (((pm >> kk) & 1ull) ? 1.f : 0.f);
           }
         } else {
           const float sc = fks[c], sh = fks[16 + c];
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk)
-            v[kk] = k2_update(xq[c][kk], ((bits >> kk) & 1u) ? dv[c][kk] : 0.f, sc, sh, a.gain, g2);
+            v[kk] = k2_update(xq[u][kk], ((bits >> kk) & 1u) ? dv[u][kk] : 0.f, sc, sh, a.gain, g2);
         }
         if (qv) {
           *reinterpret_cast<f4*>(xs + c * PSTR + 4 * q) = v;
           if (own) *reinterpret_cast<f4*>(a.xo + ((size_t)b * C + c) * HW + cell) = v;
         }
       }
+      FPROF_MARK(2);
     }
-    fbase += NQB + NW;
+    fbase += NFIT + NW;
   };
 
   // The preparer (one wave, no workgroup barrier): a tile's sender plane over the region, its keep
@@ -798,10 +820,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       }
     }
     if (lane == 0) cnt[s] = nl;
-    if constexpr (FOLD) {   // this tile's slot is complete: the finalizers may read it
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    if constexpr (FOLD) FPROF_MARK(9);
     if (GNCA_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO);
   };
 
@@ -1338,6 +1357,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     ++iter;
   }
   PROF_STORE_W03;
+  FPROF_STORE;
   GNCA_STAMP_END(a.stamps);
 }
 

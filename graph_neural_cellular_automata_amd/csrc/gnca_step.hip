@@ -76,7 +76,19 @@ __device__ unsigned long long g_prof[1024][2 * kProfPhases];   // [.][8..15]: sp
 #define PROF_STORE_W03 do { if (threadIdx.x == 0 || threadIdx.x == 192) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][(threadIdx.x ? kProfPhases : 0) + i_] = prof_acc[i_]; } while (0)
 // waves 0 and 7 (the 32-channel split K1's preparer): [.][0..7] and [.][8..15]
 #define PROF_STORE_W07 do { if (threadIdx.x == 0 || threadIdx.x == 448) for (int i_ = 0; i_ < kProfPhases; ++i_) g_prof[blockIdx.x & 1023][(threadIdx.x ? kProfPhases : 0) + i_] = prof_acc[i_]; } while (0)
+// the fold's own sub-phases (gnca_k1_split<..., FOLD>): waves 0 and 3, 16 buckets each (gnca_fprof_dump)
+__device__ unsigned long long g_fprof[1024][32];
+#define FPROF_DECL unsigned long long fp_t = __builtin_amdgcn_s_memtime(), fp_acc[16] = {0};
+#define FPROF_START() do { fp_t = __builtin_amdgcn_s_memtime(); } while (0)
+#define FPROF_MARK(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); fp_acc[i] += t_ - fp_t; fp_t = t_; } while (0)
+#define FPROF_COUNT(i) do { fp_acc[i] += 1; } while (0)
+#define FPROF_STORE do { if (threadIdx.x == 0 || threadIdx.x == 192) for (int i_ = 0; i_ < 16; ++i_) g_fprof[blockIdx.x & 1023][(threadIdx.x ? 16 : 0) + i_] = fp_acc[i_]; } while (0)
 #else
+#define FPROF_DECL
+#define FPROF_START() do {} while (0)
+#define FPROF_MARK(i) do {} while (0)
+#define FPROF_COUNT(i) do {} while (0)
+#define FPROF_STORE do {} while (0)
 #define PROF_STORE_W07 do {} while (0)
 #define PROF_STORE_W03 do {} while (0)
 #define PROF_STORE_W04 do {} while (0)
@@ -2152,6 +2164,9 @@ int gnca_perceive_f32(int32_t B, int32_t C, int32_t H, int32_t W, const float* w
 #ifdef GNCA_PROFILE
 int gnca_prof_dump(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)) == hipSuccess ? 0 : -1;
+}
+int gnca_fprof_dump(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fprof), sizeof(g_fprof)) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -15,6 +15,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "build_ablate")
 LIB = os.path.join(OUT, "lib_foldprof.so")
+FNAMES = ["fin: wait preparer", "fin: item loads + xsd wait", "fin: compute + stores", "fin: items",
+          "prep: load issue", "prep: stats + constants", "prep: alpha rows", "prep: pooling", "prep: sender plane",
+          "prep: keep + list + tables"]
 NAMES = ["stage(dma|finalize)", "prologue_wait", "gather+perc", "preparer", "group_mfma+epi", "partial_bins",
          "barrier_after_groups", "loop_top"]
 
@@ -42,6 +45,7 @@ def run():
     from graph_neural_cellular_automata_amd import step as S
     lib = L.load(LIB)
     lib.gnca_prof_dump.restype = ctypes.c_int
+    lib.gnca_fprof_dump.restype = ctypes.c_int
     dev = torch.device("cuda:0")
     wl = bench.WORKLOADS[os.environ.get("FOLDPROF_CONFIG", "headline")]
     B, H = wl["B"], wl["H"]
@@ -63,6 +67,9 @@ def run():
         buf = (ctypes.c_ulonglong * (1024 * 16))()
         assert lib.gnca_prof_dump(buf) == 0
         full = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16).astype(np.float64)
+        fb = (ctypes.c_ulonglong * (1024 * 32))()
+        assert lib.gnca_fprof_dump(fb) == 0
+        ff = np.frombuffer(fb, dtype=np.uint64).reshape(1024, 32).astype(np.float64)
         kind = "plain K1 (1-step rollout)" if steps == 1 else "fold K1 (last K1 of a 3-step rollout)"
         print(f"== {kind}: rollout {e0.elapsed_time(e1):.3f} ms (profile build), fold={S.rollout_fold(d)}")
         for title, a in (("wave 0 (SIMD 0)", full[:, :8]), ("wave 3 (preparer)", full[:, 8:])):
@@ -71,6 +78,12 @@ def run():
             print(f" {title}: mean cycles per workgroup {tot:.0f} over {len(a)} WGs")
             for i, nm in enumerate(NAMES):
                 print(f"  {nm:22s} {a[:, i].mean():12.0f} cycles  {100 * a[:, i].mean() / tot:5.1f} %")
+        if steps > 1:
+            for title, f in (("wave 0", ff[:, :16]), ("wave 3 (preparer)", ff[:, 16:])):
+                f = f[f.sum(1) > 0]
+                print(f" fold sub-phases, {title} (cycles per workgroup; items = finalize items done):")
+                for i, nm in enumerate(FNAMES):
+                    print(f"  {nm:26s} {f[:, i].mean():12.0f}")
 
 
 if __name__ == "__main__":
