@@ -550,10 +550,13 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       lv[r] = 1u;   // dense field: every value is used (a dead cell's is 0)
       if constexpr (CF) lv[r] = (uint32_t)(*reinterpret_cast<const uint64_t*>(&fts[r * 3 + kcol]) >> tjS) & 1u;
     }
+    // (every row's updated alpha first: independent chains the scheduler interleaves; then the
+    //  ballots, each row's stored right away)
+#pragma unroll
+    for (int r = 0; r < PBH; ++r) xv[r] = fin_alpha(xv[r], lv[r] != 0 ? dv[r] : 0.f, mu, rs, g3, b3, a.gain, gn);
 #pragma unroll
     for (int r = 0; r < PBH; ++r) {
-      const bool live = lv[r] != 0;
-      const float xa = fin_alpha(xv[r], live ? dv[r] : 0.f, mu, rs, g3, b3, a.gain, gn);
+      const float xa = xv[r];
       const uint64_t b0 = __ballot(lin && xa > a.alpha_thr), b1 = __ballot(lin && xa > a.graph_alpha_thr);
       if (lane == 0) {   // stored right away: no scalar pair stays live past its row
         pbm[r] = b0;
@@ -688,26 +691,31 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       FPROF_COUNT(3);
       const bool own = vr >= RY && vr < RY + TH && vq >= RX / 4 && vq < (RX + TW) / 4;
       const uint64_t pm = p0s[vr] >> (4 * vq + 4);
+      // every channel's values in one straight block (no per-channel branch), then the stores
 #pragma unroll
       for (int u = 0; u < FCH; ++u) {
         const int c = c0 + u;
-        f4 v;
         if (c == 3) {
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
             const float xa = fin_alpha(xq[u][kk], ((bits >> kk) & 1u) ? dv[u][kk] : 0.f, mu, rs, g3, b3, a.gain, gn);
-            v[kk] = xa * (((pm >> kk) & 1ull) ? 1.f : 0.f);
+            xq[u][kk] = xa * (((pm >> kk) & 1ull) ? 1.f : 0.f);
           }
         } else {
           const float sc = fks[c], sh = fks[16 + c];
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk)
-            v[kk] = k2_update(xq[u][kk], ((bits >> kk) & 1u) ? dv[u][kk] : 0.f, sc, sh, a.gain, g2);
+            xq[u][kk] = k2_update(xq[u][kk], ((bits >> kk) & 1u) ? dv[u][kk] : 0.f, sc, sh, a.gain, g2);
         }
-        if (qv) {
-          *reinterpret_cast<f4*>(xs + c * PSTR + 4 * q) = v;
-          if (own) *reinterpret_cast<f4*>(a.xo + ((size_t)b * C + c) * HW + cell) = v;
-        }
+      }
+      // lanes past the region write their quad into the (unused) alive-byte area instead: no branch
+      float* const xdummy = reinterpret_cast<float*>(smem_b + L.ab) + 4 * (lane & 15);
+#pragma unroll
+      for (int u = 0; u < FCH; ++u) *reinterpret_cast<f4*>(qv ? xs + (c0 + u) * PSTR + 4 * q : xdummy) = xq[u];
+      if (own && qv) {
+        float* ob = a.xo + ((size_t)b * C + c0) * HW + cell;
+#pragma unroll
+        for (int u = 0; u < FCH; ++u) *reinterpret_cast<f4*>(ob + (size_t)u * HW) = xq[u];
       }
       FPROF_MARK(2);
     }
