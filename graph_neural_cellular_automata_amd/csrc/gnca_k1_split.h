@@ -371,7 +371,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   wg_stamp(a.stamps, 0);
   FPROF_DECL
   if constexpr (FOLD) {   // the fold's counters are used before the prologue's barrier
-    if (tid == 0) { *fctr = 0; *pdone = 0; }
+    if (tid == 0) { *fctr = 0; *pdone = 0; cnt[6] = 0; cnt[7] = 0; }
     __syncthreads();
   }
   if (GNCA_K1_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO);
@@ -613,7 +613,11 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   // the row tables come from the slot) are issued before the wait for the staging buffer to be free
   // (every group of the current tile past its staged reads), so they overlap the other waves' last
   // groups.
-  auto finalize = [&](int t, int s, int need_prep, bool wait_xsd, int qe, int xb) {
+  // wait_xsd: the staging buffer still holds the current tile (groups qe, live list lstc, group
+  // done-mask cnt[6 + parc]): an item overwrites its rows once every group that may read them is past
+  // its staged reads (the groups' cells are in row order, so the top rows free up first)
+  static_assert(!FOLD || NG <= 32, "one done bit per group");
+  auto finalize = [&](int t, int s, int need_prep, bool wait_xsd, int qe, const uint16_t* lstc, int parc) {
     const int b = t / a.tps, tin = t - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
@@ -630,7 +634,8 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     int gc0 = j0 - RX;
     gc0 = gc0 < 0 ? gc0 + W : gc0;
     const int tx0 = gc0 / TW;
-    bool waited = !wait_xsd;
+    // lane q: the tile row of group q's first cell (the least row it reads, in region rows)
+    const int grow = (wait_xsd && lane < qe) ? lstc[32 * lane] / TW : 0;
 #pragma unroll 1
     for (;;) {
       const int it = (__builtin_amdgcn_readfirstlane(atomicAdd(fctr, 1)) >> 6) - fbase;
@@ -682,10 +687,11 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
           for (int kk = 0; kk < 4; ++kk) dv[u][kk] = d4[kk];
         }
       }
-      if (!waited) {
-        while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xb < qe)
+      if (wait_xsd) {
+        const int rhi = min(RH - 1, (64 * (it / (C / FCH)) + 63) / QW);   // the item's last region row
+        const uint32_t need = (uint32_t)__ballot(lane < qe && grow <= rhi);
+        while ((__hip_atomic_load(cnt + 6 + parc, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) & need) != need)
           __builtin_amdgcn_s_sleep(1);
-        waited = true;
       }
       FPROF_MARK(1);
       FPROF_COUNT(3);
@@ -864,7 +870,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   }
   PROF_MARK(2);   // (prologue) weight image copy / fill issue
   if constexpr (FOLD) {   // the first tile's region: finalized by every wave (nothing to wait for)
-    if (tile < t_end) finalize(tile, 0, 1, false, 0, 0);
+    if (tile < t_end) finalize(tile, 0, 1, false, 0, nullptr, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PROF_MARK(1);   // (prologue) wait for the DMA, images and weight loads
@@ -1037,6 +1043,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       split3_x8(y2, yf[2][0], yf[2][1], yf[2][2]);
       // this group's reads of the staged planes are done (release: they stay before the count)
       __hip_atomic_fetch_add(xsd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if constexpr (FOLD) __hip_atomic_fetch_or(cnt + 6 + par, 1 << q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       PROF_MARK(2);   // pull + gather + perception + splits
       if (GNCA_K1_DYNPRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO + GNCA_K1_DYNPRIO);
       if (GNCA_ABLATE & kAblMfma) {
@@ -1340,7 +1347,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     // still run their last groups' MFMAs and stores.
     if constexpr (FOLD) {
       // every wave: the next tile's region finalized into the staging buffer (+ its cells into xo)
-      if (nxt < t_end) finalize(nxt, par ^ 1, iter + 2, true, qend, xbase);
+      if (nxt < t_end) finalize(nxt, par ^ 1, iter + 2, true, qend, lst, par);
     } else if (q >= qend && q < qend + GNCA_DMA_WAVES && nxt < t_end) {
       while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xbase < qend)
         __builtin_amdgcn_s_sleep(1);
@@ -1352,6 +1359,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     PROF_MARK(6);
     gbase += qend + NW;
     xbase += qend;
+    if constexpr (FOLD) if (tid == 0) cnt[6 + par] = 0;   // this tile's group done-mask, for tile + 2
     // ---- the tile's GroupNorm partials in 8 bins (bin j: groups j, j + 8, ... in order; K2 sums the
     //      bins of a sample in fixed order) ----
     if (tid < 2 * NW) {
