@@ -80,6 +80,7 @@ PHASE_ALL = 7
 PHASE_ALIVE = 8   # rollout mode: K2 hands the next step's alive masks to K1 (include/gnca.h)
 ROLLOUT_ALIVE_IN, ROLLOUT_ALIVE_OUT = 1, 2   # gnca_rollout_ex_f32 pieces (include/gnca.h)
 ROLLOUT_PENDING_IN, ROLLOUT_PENDING_OUT = 4, 8   # fold rollouts: the last step handed over unfinished
+ROLLOUT_FOLD = 16   # request the fold on the compact field too (include/gnca.h)
 PHASE_COMPACT = 16   # rollout mode: K1 packs the live cells' dx per tile, K2 unpacks (include/gnca.h)
 
 _lib = None

@@ -301,6 +301,10 @@ __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst)
   else ks_fill_images<512, false, false>(a, dst, threadIdx.x);
 }
 
+#ifndef GNCA_FOLD_ABL
+#define GNCA_FOLD_ABL 0   // timing-only builds: 1 = the finalize's loads hit a few cached lines instead
+#endif
+
 #ifndef GNCA_K1_SPLIT_NT
 #define GNCA_K1_SPLIT_NT 512   // threads per workgroup of the 16-channel split K1 (768: 3 waves per SIMD)
 #endif
@@ -649,8 +653,14 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       gc = gc < 0 ? gc + W : (gc >= W ? gc - W : gc);
       const size_t cell = (size_t)g * W + gc;
       f4 xq[FCH];
+#if GNCA_FOLD_ABL & 1   // timing only: no finalize loads (wrong results)
+      const size_t cell_ = (size_t)(lane & 3);
+#define GNCA_FCELL cell_
+#else
+#define GNCA_FCELL cell
+#endif
 #pragma unroll
-      for (int u = 0; u < FCH; ++u) xq[u] = *reinterpret_cast<const f4*>(a.xp + ((size_t)b * C + c0 + u) * HW + cell);
+      for (int u = 0; u < FCH; ++u) xq[u] = *reinterpret_cast<const f4*>(a.xp + ((size_t)b * C + c0 + u) * HW + GNCA_FCELL);
       float dv[FCH][4];
       uint32_t bits = 15u;   // dense field: every value is used (a dead cell's is 0)
       if constexpr (CF) {
@@ -665,12 +675,12 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         const uint32_t r0 = e[3] * (uint32_t)(C * NCELL) + e[2] + (uint32_t)__popcll(m & ((1ull << tjS) - 1ull));
         uint32_t off[4];
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) off[kk] = r0 + (uint32_t)__popc(bits & ((1u << kk) - 1u));
+        for (int kk = 0; kk < 4; ++kk) off[kk] = (GNCA_FOLD_ABL & 1) ? (uint32_t)(lane & 3) : r0 + (uint32_t)__popc(bits & ((1u << kk) - 1u));
 #pragma unroll
         for (int u = 0; u < FCH; ++u) {
           const int c = c0 + u;
           if (c == 3) {
-            const f4 d4 = *reinterpret_cast<const f4*>(a.dxap + (size_t)b * HW + cell);
+            const f4 d4 = *reinterpret_cast<const f4*>(a.dxap + (size_t)b * HW + GNCA_FCELL);
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) dv[u][kk] = d4[kk];
           } else {
@@ -682,7 +692,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       } else {
 #pragma unroll
         for (int u = 0; u < FCH; ++u) {
-          const f4 d4 = *reinterpret_cast<const f4*>(a.dxp + ((size_t)b * C + c0 + u) * HW + cell);
+          const f4 d4 = *reinterpret_cast<const f4*>(a.dxp + ((size_t)b * C + c0 + u) * HW + GNCA_FCELL);
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) dv[u][kk] = d4[kk];
         }

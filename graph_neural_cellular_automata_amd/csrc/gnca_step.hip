@@ -1461,7 +1461,8 @@ struct Plan {
   // the fold (rollouts of a fold-capable K1 on the compact field): K1 of step t also finishes step
   // t - 1, so the compact field (dx, row tables, alpha plane, partials) is double-buffered by the
   // parity of the global step index: set 1 at off_*2
-  bool fold_ok;
+  bool fold_ok;    // planned for rollouts by default (the dense field: small batches)
+  bool fold_any;   // possible (also on the compact field, on request: GNCA_ROLLOUT_FOLD)
   size_t off_dx2, off_stats2, off_rmask2, off_rpre2, off_dxa2;
 };
 
@@ -1625,13 +1626,20 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // the compact field (each field + 256 B: the finalizer's quad reads may touch one float past it)
   // (the update field is compact for large batches and dense NCHW for small ones)
   // (the preparer sums a sample's partials in one wave pass: tps * waves <= 256)
-  P->fold_ok = P->var->fold_fn[P->compact_ok ? 1 : 0] != nullptr && !msg_only && !attn_on &&
+  // The fold on the compact field (large batches) is built and bitwise-tested but not planned by
+  // default: measured on the headline (B=1024 72^2) it runs 0.566 ms/step against 0.504 for the
+  // sub-batch pipeline (K1 + K2 on two streams), because the finalize of each tile's 1.63x halo
+  // region comes after the tile's groups and waits on its loads ("The fold").  Small
+  // batches (dense field) fold: one launch per step instead of two (BASELINE c2 18.6 -> 15.7 us,
+  // c3 20.4 -> 18.3 us).  A rollout asks for the compact fold with GNCA_ROLLOUT_FOLD (fold_any).
+  P->fold_any = P->var->fold_fn[P->compact_ok ? 1 : 0] != nullptr && !msg_only && !attn_on &&
                (P->graph_on ? P->k == P->var->KU : P->var->KU == 0) &&
                d->alpha_thr >= 0.f && d->graph_alpha_thr >= d->alpha_thr && n < (size_t)1 << 31 &&
                P->tps * P->ppt <= 256;
-  const bool fc = P->fold_ok && P->compact_ok;
-  P->off_dx2 = carve(P->fold_ok ? n * 4 + 256 : 0);
-  P->off_stats2 = carve(P->fold_ok ? (size_t)P->total_tiles * P->ppt * 2 * sizeof(double) : 0);
+  P->fold_ok = P->fold_any && !P->compact_ok;
+  const bool fc = P->fold_any && P->compact_ok;
+  P->off_dx2 = carve(P->fold_any ? n * 4 + 256 : 0);
+  P->off_stats2 = carve(P->fold_any ? (size_t)P->total_tiles * P->ppt * 2 * sizeof(double) : 0);
   P->off_rmask2 = carve(fc ? (size_t)P->total_tiles * P->TH * sizeof(uint64_t) : 0);
   P->off_rpre2 = carve(fc ? (size_t)P->total_tiles * P->TH * sizeof(uint32_t) : 0);
   P->off_dxa2 = carve(fc ? (size_t)d->B * d->H * d->W * sizeof(float) : 0);
@@ -1819,7 +1827,7 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   if (want_attn && !attn) return GNCA_ERR_INVALID;
   if (!ws || ws_bytes < P.ws_bytes) return GNCA_ERR_WORKSPACE;
   char* wsb = reinterpret_cast<char*>(ws);
-  if (set != 0 && !P.fold_ok) return GNCA_ERR_INVALID;
+  if (set != 0 && !P.fold_any) return GNCA_ERR_INVALID;
   const FieldSet fs = field_set(P, wsb, set);
   int rc;
   if ((phases & GNCA_PHASE_K0) && P.need_k0 && (rc = launch_k0(d, w, P, x, wsb, st)) != GNCA_OK)
@@ -1988,7 +1996,7 @@ static void sub_desc(const gnca_step_desc* d, int sub, int nsub, gnca_step_desc*
 static int rollout_subs(const gnca_step_desc* d) {
   if (kRolloutSubs < 2 || !d || d->B < kRolloutSubs) return 1;
   Plan P;
-  if (!make_plan(d, false, &P) || P.var->split != 1 || !P.compact_ok || P.fold_ok) return 1;
+  if (!make_plan(d, false, &P) || P.var->split != 1 || !P.compact_ok || P.fold_ok) return 1;   // (fold_ok: dense)
   for (int s = 0; s < kRolloutSubs; ++s) {
     gnca_step_desc sd;
     int b0;
@@ -2083,7 +2091,7 @@ int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* 
     snprintf(name, (size_t)n, "gnca_k1_update<%d,%d,%d,%d,%d,%d,%d,%d>", v->CP, v->HDP, v->TH, v->TW, v->RY, v->RX,
              v->KU, v->NT);
   if (arith) *arith = (v->split ? 1 : 0) | (P.compact_ok ? 2 : 0) | (rollout_subs(desc) > 1 ? 4 : 0) |
-                      (P.fold_ok ? 8 : 0);
+                      (P.fold_ok ? 8 : 0) | (P.fold_any ? 16 : 0);
   return GNCA_OK;
 }
 
@@ -2190,7 +2198,7 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
                         uint32_t flags) {
   if (!desc || steps < 0 || !x || !x_final || !scratch) return GNCA_ERR_INVALID;
   if (flags & ~(uint32_t)(GNCA_ROLLOUT_ALIVE_IN | GNCA_ROLLOUT_ALIVE_OUT | GNCA_ROLLOUT_PENDING_IN |
-                          GNCA_ROLLOUT_PENDING_OUT))
+                          GNCA_ROLLOUT_PENDING_OUT | GNCA_ROLLOUT_FOLD))
     return GNCA_ERR_INVALID;
   if ((flags & GNCA_ROLLOUT_ALIVE_IN) && (flags & GNCA_ROLLOUT_PENDING_IN)) return GNCA_ERR_INVALID;
   if ((flags & GNCA_ROLLOUT_ALIVE_OUT) && (flags & GNCA_ROLLOUT_PENDING_OUT)) return GNCA_ERR_INVALID;
@@ -2218,7 +2226,7 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
   const int nsub = rollout_subs(&dt);
   Plan PF;
   if (!make_plan(&dt, false, &PF)) return GNCA_ERR_INVALID;
-  const bool fold = PF.fold_ok && nsub == 1;
+  const bool fold = (PF.fold_ok && nsub == 1) || (PF.fold_any && (flags & GNCA_ROLLOUT_FOLD));
   if ((pend_in || pend_out) && !fold) return GNCA_ERR_INVALID;
   // the 16-channel split K1's weight images, once for the whole rollout (every K1 launch then copies
   // them into LDS with LDS-DMA instead of loading, splitting and storing the fp32 weights)

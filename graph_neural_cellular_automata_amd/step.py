@@ -158,14 +158,15 @@ def rollout_subs(desc: L.StepDesc) -> int:
     return 2 if arith.value & 4 else 1
 
 
-def rollout_fold(desc: L.StepDesc) -> bool:
-    """True when a rollout of ``desc``'s shape folds each step's finalize (GroupNorm, tanh * gain,
+def rollout_fold(desc: L.StepDesc, possible: bool = False) -> bool:
+    """True when a rollout of ``desc``'s shape folds each step's finish (GroupNorm, tanh * gain,
     residual, post-update alpha gate) into the next step's K1, so one K1 launch per step plus one
-    K2 at the end of the rollout (gnca_k1_variant arith bit 8)."""
+    K2 at the end of the rollout (gnca_k1_variant arith bit 8).  ``possible``: whether it can, on
+    request (``rollout(..., fold=True)``; arith bit 16) where it is not the default."""
     buf = ctypes.create_string_buffer(128)
     arith = ctypes.c_int32(0)
     L.check(L.load().gnca_k1_variant(ctypes.byref(desc), buf, 128, ctypes.byref(arith)), "gnca_k1_variant")
-    return bool(arith.value & 8)
+    return bool(arith.value & (16 if possible else 8))
 
 
 def stream_ptr(device) -> int:
@@ -241,8 +242,9 @@ def fire_mask(desc, device) -> torch.Tensor:
     return m
 
 
-def rollout(desc, weights, x, steps: int, offsets_per_step: list):
-    """``steps`` no-grad steps (GNCA_FIRE_HASH / NONE) in one C call."""
+def rollout(desc, weights, x, steps: int, offsets_per_step: list, fold: bool = False):
+    """``steps`` no-grad steps (GNCA_FIRE_HASH / NONE) in one C call.  ``fold``: fold each step's
+    finish into the next K1 even where that is not the default (GNCA_ROLLOUT_FOLD)."""
     lib = L.load()
     k = desc.num_offsets
     flat = [v for offs in offsets_per_step for o in offs for v in o]
@@ -252,10 +254,10 @@ def rollout(desc, weights, x, steps: int, offsets_per_step: list):
     out = torch.empty_like(x)
     scratch = torch.empty_like(x)
     ws = workspace(desc, x.device)
-    rc = lib.gnca_rollout_f32(ctypes.byref(desc), ctypes.byref(weights), int(steps), arr,
-                              x.data_ptr(), out.data_ptr(), scratch.data_ptr(), ws.data_ptr(),
-                              ws.numel(), stream_ptr(x.device))
-    L.check(rc, "gnca_rollout_f32")
+    rc = lib.gnca_rollout_ex_f32(ctypes.byref(desc), ctypes.byref(weights), int(steps), arr,
+                                 x.data_ptr(), out.data_ptr(), scratch.data_ptr(), ws.data_ptr(),
+                                 ws.numel(), L.ROLLOUT_FOLD if fold else 0, stream_ptr(x.device))
+    L.check(rc, "gnca_rollout_ex_f32")
     return out
 
 

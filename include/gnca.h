@@ -123,7 +123,8 @@ size_t gnca_workspace_bytes(const gnca_step_desc* desc);
  * (GNCA_PHASE_COMPACT), plus 4 when a rollout of this shape runs as 2 concurrent sub-batches (one
  * stream each: one sub-batch's K2 beside the other's K1; see gnca_rollout_f32), plus 8 when a
  * rollout of this shape folds each step's finish (GroupNorm, tanh, residual, alpha gate) into the
- * next step's K1 (one K1 launch per step and one K2 at the end).  Host-only.
+ * next step's K1 (one K1 launch per step and one K2 at the end), plus 16 when such a fold is
+ * possible for this shape (on request, GNCA_ROLLOUT_FOLD, where it is not the default).  Host-only.
  * Returns GNCA_OK or GNCA_ERR_INVALID. */
 int gnca_k1_variant(const gnca_step_desc* desc, char* name, int32_t n, int32_t* arith);
 
@@ -225,6 +226,9 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
  */
 #define GNCA_ROLLOUT_PENDING_IN  (1u << 2)
 #define GNCA_ROLLOUT_PENDING_OUT (1u << 3)
+/* Fold even on the compact update field (gnca_k1_variant arith bit 16): large batches otherwise run
+ * the two-stream sub-batch pipeline, which measured faster on MI355X ("The fold"). */
+#define GNCA_ROLLOUT_FOLD        (1u << 4)
 int gnca_rollout_ex_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
                         const int8_t* offsets, const float* x, float* x_final, float* scratch,
                         void* ws, size_t ws_bytes, uint32_t flags, void* stream);

@@ -196,8 +196,10 @@ def test_compact_rollout_equals_dense_steps(dev, graph):
 
     name, arith = S.k1_variant(desc(0))
     assert arith == "bf16x6", name
-    assert S.rollout_fold(desc(0))   # each step's finish is folded into the next step's K1
+    assert not S.rollout_fold(desc(0)) and S.rollout_fold(desc(0), possible=True)
     r = S.rollout(desc(0), w, x.contiguous(), steps, offs)
+    # the fold on request (each finish inside the next K1, the compact field double-buffered)
+    assert torch.equal(S.rollout(desc(0), w, x.contiguous(), steps, offs, fold=True), r)
     cur = x
     for t in range(steps):
         cur, _ = S.step(desc(t), w, cur)
@@ -516,9 +518,11 @@ def test_fold_rollout_pieces_bitwise(dev, B, graph):
                            update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
                            fire_mode=L.FIRE_HASH, rng_seed=11, rng_step=t, sample_base=3)
 
-    assert S.rollout_fold(desc(0)) and S.rollout_subs(desc(0)) == 1
-    assert S.rollout_compact(desc(0)) == (B > 8)
-    one = S.rollout(desc(0), w, x.contiguous(), steps, offs)
+    compact = B > 8
+    assert S.rollout_compact(desc(0)) == compact
+    # small batches fold by default; the compact field folds on request (GNCA_ROLLOUT_FOLD)
+    assert S.rollout_fold(desc(0)) == (not compact) and S.rollout_fold(desc(0), possible=True)
+    one = S.rollout(desc(0), w, x.contiguous(), steps, offs, fold=True)
     cur = x
     for t in range(steps):
         cur, _ = S.step(desc(t), w, cur)
@@ -532,7 +536,8 @@ def test_fold_rollout_pieces_bitwise(dev, B, graph):
         src, s0 = x.contiguous(), 0
         outs = [torch.empty_like(x), torch.empty_like(x)]
         for i, n in enumerate(sizes):
-            fl = (L.ROLLOUT_PENDING_IN if i > 0 else 0) | (L.ROLLOUT_PENDING_OUT if i + 1 < len(sizes) else 0)
+            fl = (L.ROLLOUT_PENDING_IN if i > 0 else 0) | (L.ROLLOUT_PENDING_OUT if i + 1 < len(sizes) else 0) | \
+                (L.ROLLOUT_FOLD if compact else 0)
             flat = [v for o in offs[s0:s0 + n] for p in o for v in p]
             arr = (ctypes.c_int8 * len(flat))(*flat) if flat else None
             dst = outs[i % 2]
@@ -549,7 +554,8 @@ def test_fold_rollout_pieces_bitwise(dev, B, graph):
     if not (graph and B > 8):
         return
     arr = (ctypes.c_int8 * 16)(*[v for p in offs[0] for v in p])
-    for fl in (L.ROLLOUT_PENDING_OUT | L.ROLLOUT_ALIVE_OUT, L.ROLLOUT_PENDING_IN | L.ROLLOUT_ALIVE_IN):
+    for fl in (L.ROLLOUT_PENDING_OUT | L.ROLLOUT_ALIVE_OUT, L.ROLLOUT_PENDING_IN | L.ROLLOUT_ALIVE_IN,
+               L.ROLLOUT_PENDING_OUT):   # (the last: no fold without GNCA_ROLLOUT_FOLD on the compact field)
         assert lib.gnca_rollout_ex_f32(ctypes.byref(desc(0)), ctypes.byref(w), 1, arr, x.data_ptr(),
                                        scratch.data_ptr(), torch.empty_like(x).data_ptr(), ws.data_ptr(),
                                        ws.numel(), fl, st) == -1
@@ -557,7 +563,7 @@ def test_fold_rollout_pieces_bitwise(dev, B, graph):
                      flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
                      update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
                      fire_mode=L.FIRE_HASH, rng_seed=11)
-    assert not S.rollout_fold(d8)   # 40^2: the 8x20 K1 has no fold variant
+    assert not S.rollout_fold(d8, possible=True)   # 40^2: the 8x20 K1 has no fold variant
     x8 = _state(8, 16, 40, 40, dev, seed=2)
     ws8 = S.workspace(d8, dev)
     assert lib.gnca_rollout_ex_f32(ctypes.byref(d8), ctypes.byref(w), 1, arr, x8.data_ptr(),

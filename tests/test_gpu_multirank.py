@@ -62,7 +62,7 @@ def test_two_rank_sharded_rollout_bitwise_equals_one_rank(dev, tmp_path):
     ref, plan = M.hip_rollout(spec, M.roll_state(spec), 0, dev)
     print(f"[multirank] rollout plans: ranks {res['plans']}, one rank {plan}")
     assert res["plans"][0][0] == "gnca_k1_split<24,36,4,4,8>" and res["plans"][0][1], res["plans"]
-    assert res["plans"][0][3], "C4's per-GPU shard folds each step's finish into the next K1"
+    assert res["plans"][0][2] == 1 and not res["plans"][0][3], "C4's shard: one stream, no fold"
     assert torch.equal(gathered, ref.cpu())
 
 

@@ -14,7 +14,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "build_ablate")
-LIB = os.path.join(OUT, "lib_foldprof.so")
+LIB = os.path.join(OUT, os.environ.get("FOLDPROF_LIB", "lib_foldprof.so"))
+EXTRA = os.environ.get("FOLDPROF_DEFS", "").split()   # build: extra -D flags (timing-only ablations)
 FNAMES = ["fin: wait preparer", "fin: item loads + xsd wait", "fin: compute + stores", "fin: items",
           "prep: load issue", "prep: stats + constants", "prep: alpha rows", "prep: pooling", "prep: sender plane",
           "prep: keep + list + tables"]
@@ -28,8 +29,8 @@ def build():
            ("gnca_step.hip", "gnca_bwd.hip", "gnca_aux.hip")]
     objs = []
     for s in src:
-        o = os.path.join(OUT, os.path.basename(s) + ".prof.o")
-        extra = ["-fno-slp-vectorize", "-DGNCA_PROFILE"] if s.endswith("gnca_step.hip") else []
+        o = os.path.join(OUT, os.path.basename(s) + "." + os.path.basename(LIB) + ".o")
+        extra = ["-fno-slp-vectorize", "-DGNCA_PROFILE", *EXTRA] if s.endswith("gnca_step.hip") else []
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
                         *extra, f"-I{ROOT}/include", s, "-o", o], check=True, stderr=subprocess.DEVNULL)
         objs.append(o)
