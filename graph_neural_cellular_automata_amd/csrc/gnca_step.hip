@@ -2223,10 +2223,12 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
   if ((flags & (GNCA_ROLLOUT_ALIVE_IN | GNCA_ROLLOUT_ALIVE_OUT)) && !hand_alive) return GNCA_ERR_INVALID;
   const bool in0 = (flags & GNCA_ROLLOUT_ALIVE_IN) != 0, out_last = (flags & GNCA_ROLLOUT_ALIVE_OUT) != 0;
   const bool pend_in = (flags & GNCA_ROLLOUT_PENDING_IN) != 0, pend_out = (flags & GNCA_ROLLOUT_PENDING_OUT) != 0;
-  const int nsub = rollout_subs(&dt);
   Plan PF;
   if (!make_plan(&dt, false, &PF)) return GNCA_ERR_INVALID;
-  const bool fold = (PF.fold_ok && nsub == 1) || (PF.fold_any && (flags & GNCA_ROLLOUT_FOLD));
+  // the fold runs the whole batch on one stream (a requested fold overrides the sub-batch pipeline,
+  // whose workspace carve differs: the weight images below must use the fold's)
+  const bool fold = PF.fold_ok || (PF.fold_any && (flags & GNCA_ROLLOUT_FOLD));
+  const int nsub = fold ? 1 : rollout_subs(&dt);
   if ((pend_in || pend_out) && !fold) return GNCA_ERR_INVALID;
   // the 16-channel split K1's weight images, once for the whole rollout (every K1 launch then copies
   // them into LDS with LDS-DMA instead of loading, splitting and storing the fp32 weights)
