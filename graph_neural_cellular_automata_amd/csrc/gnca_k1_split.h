@@ -166,7 +166,7 @@ __host__ __device__ constexpr int ks_a16(int v) { return (v + 15) & ~15; }
 // The planes a tile's groups read besides the staged channel planes (the sender plane sp over the
 // region and the live-cell list) come in two slots: the preparer wave fills the next tile's slot
 // while the other waves still run this tile's groups (below).
-template <int TH, int TW, int RY, int RX>
+template <int TH, int TW, int RY, int RX, bool FOLD = false>
 __host__ __device__ constexpr KSLayout ks_layout() {
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
   KSLayout L{};
@@ -178,17 +178,18 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   L.ab = o; o += ks_a16(RHW);             // the preparer's alive bytes over the region
   L.lst = o; o += 2 * L.lst_slot;         // live-cell list (u16 cell indices), two slots
   L.cnt = o; o += 32;                     // live cells per slot; group counter; staging-reads-done counter;
-                                          // fold: finalize-item counter, preparations done
+                                          // fold: finalize-item counter, preparations done, group done-masks
   L.cb = o; o += ks_a16(8 * (TH * TW / 64 + 2));   // the preparer's 64-cell chunk ballots
   L.pg = o; o += 2 * 16 * ((TH * TW + 31) / 32);  // per-group GroupNorm partials (fp64 pairs), two slots
   // fold (gnca_k1_split<..., FOLD>): per slot the previous step's GroupNorm constants (48 floats) and
   // the region's pre-update alive row masks P0 (one u64 per region row); the preparer's sender row
   // masks P1 and its threshold-bit row masks of the pooled band (2 x (RH + 2) u64)
-  L.fk = o; o += 2 * 192;
-  L.p0 = o; o += 2 * ks_a16(RH * 8);
-  L.p1 = o; o += ks_a16(RH * 8);
-  L.pbm = o; o += ks_a16(2 * (RH + 2) * 8);
-  L.ft = o; o += 2 * ks_a16((RH + 2) * 3 * 16);   // per slot: the previous step's row tables of the band's source tiles
+  // (only in the fold variant's layout: the plain K1 keeps room for a co-resident K2 workgroup)
+  L.fk = o; o += FOLD ? 2 * 192 : 0;
+  L.p0 = o; o += FOLD ? 2 * ks_a16(RH * 8) : 0;
+  L.p1 = o; o += FOLD ? ks_a16(RH * 8) : 0;
+  L.pbm = o; o += FOLD ? ks_a16(2 * (RH + 2) * 8) : 0;
+  L.ft = o; o += FOLD ? 2 * ks_a16((RH + 2) * 3 * 16) : 0;   // per slot: the previous step's row tables
   L.w1 = o; o += 3 * 4 * 3 * 1024;       // [plane][rb][kc][lane] x 16 B
   L.bias = o; o += 4 * 32 * 16;          // [rb][row] x 16 B (k slots 0..2 = the three parts)
   L.w2 = o; o += 3 * 8 * 2 * 16 * 16;    // [plane][s][h][channel] x 16 B
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   constexpr int NQ = RHW / 4, NI4 = (NQ + 63) / 64;
   constexpr int QW = RW / 4, NQA = RH * QW;
   constexpr int NCELL = TH * TW;
-  constexpr KSLayout L = ks_layout<TH, TW, RY, RX>();
+  constexpr KSLayout L = ks_layout<TH, TW, RY, RX, FOLD != 0>();
   static_assert(RW % 4 == 0 && RX % 4 == 0 && TW % 4 == 0, "16-byte staging rows");
   static_assert(RY >= 1 && RX >= 1, "perception halo");
   static_assert(L.total + 512 <= 160 * 1024, "LDS (+ the compiler's static LDS, e.g. __syncthreads_and)");

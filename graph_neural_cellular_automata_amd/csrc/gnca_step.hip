@@ -1395,20 +1395,22 @@ struct Variant {
   int lds_split;                     // its LDS bytes (compile-time layout)
   const void* fold_fn[2];            // the same K1 that also finishes the previous step (rollouts) on the
                                      // [dense, compact] update field, or null
+  int lds_fold;                      // the fold variant's LDS bytes
 };
 
-#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0, {nullptr, nullptr}}
+#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0, {nullptr, nullptr}, 0}
 #define GNCA_SV(th, tw, ry, rx, ku) \
   {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
-   ks_layout<th, tw, ry, rx>().total, {nullptr, nullptr}}
+   ks_layout<th, tw, ry, rx>().total, {nullptr, nullptr}, 0}
 // fold variants: the large-batch tile (dense: nullptr, it is only planned with the compact field) and
 // the small-batch ones (both layouts)
 #define GNCA_SVF(th, tw, ry, rx, ku, dense) \
   {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
-   ks_layout<th, tw, ry, rx>().total, {dense, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku, 2>)}}
+   ks_layout<th, tw, ry, rx>().total, {dense, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku, 2>)}, \
+   ks_layout<th, tw, ry, rx, true>().total}
 #define GNCA_S32V(th, tw, ry, rx, ku) \
   {32, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split32<th, tw, ry, rx, ku>), 512, 2, \
-   ks32_layout<th, tw, ry, rx>().total, {nullptr, nullptr}}
+   ks32_layout<th, tw, ry, rx>().total, {nullptr, nullptr}, 0}
 static const Variant kVariants[] = {
     // 16 channels, hidden 128, bf16 MFMA on exact 3-way splits (gnca_k1_split.h), compile-time
     // geometry: list order is the large-batch preference (24x36: the largest tiles whose halo fits
@@ -1941,12 +1943,13 @@ static int fold_k1(const gnca_step_desc* d, const gnca_weights* w, const Plan& P
   k1.wimg = wimg;
   k1.stamps = stamps;
   const void* fn = P.var->fold_fn[P.compact_ok ? 1 : 0];
-  const int occ = occupancy(fn, P.lds1, P.var->NT);
+  const size_t lds = (size_t)P.var->lds_fold;
+  const int occ = occupancy(fn, lds, P.var->NT);
   long grid = std::min<long>((long)device_cus() * occ, P.total_tiles);
   if (grid < 1) grid = 1;
   if (stamps && grid > stamp_cap) return GNCA_ERR_INVALID;
   void* args[] = {&k1};
-  const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(P.var->NT), args, P.lds1, st);
+  const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(P.var->NT), args, lds, st);
   if (e != hipSuccess) {
     g_last_hip = (int)e;
     return GNCA_ERR_HIP;
