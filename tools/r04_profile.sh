@@ -2,7 +2,7 @@
 # Round-4 evidence for the bench line, each GPU step under its own limit, stopping at the first
 # failure: (1) rocprofv3 kernel trace + stats of exactly the driver's command, summarised over the
 # timed rollout's own launches (tools/timed_kernels.py); (2) the PMC passes (tools/pmc.sh) ->
-# per-launch HBM traffic and MFMA busy of the fold K1 (tools/pmc_traffic.py).
+# per-launch HBM traffic and MFMA busy of K1 (two sub-batch launches per step) (tools/pmc_traffic.py).
 #   TAG=r04a bash tools/r04_profile.sh [prof] [pmc]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -23,7 +23,7 @@ for s in "$@"; do
       PMC_CMD="python3 bench.py --steps 4 --warmup 1 --no-cpu --gpu-warmup-ms 0" PMC_OUT=gpurun_out/pmc_$TAG \
         bash tools/pmc.sh > gpurun_out/pmc_$TAG.log 2>&1
       rc=$?; echo "pmc rc=$rc"; [ $rc -ne 0 ] && { tail -20 gpurun_out/pmc_$TAG.log; exit $rc; }
-      PMC_LAUNCHES_PER_STEP=1 python3 tools/pmc_traffic.py gpurun_out/pmc_$TAG gpurun_out/${TAG}_pmc_traffic.json
+      PMC_LAUNCHES_PER_STEP=2 python3 tools/pmc_traffic.py gpurun_out/pmc_$TAG gpurun_out/${TAG}_pmc_traffic.json
       python3 tools/pmc_summary.py gpurun_out/pmc_$TAG > gpurun_out/${TAG}_pmc_summary.txt
       head -60 gpurun_out/${TAG}_pmc_summary.txt ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -11,12 +11,13 @@ the bench line's ms_per_step and its stamp-based K1 duration.
 """
 import csv
 import json
+import re
 import sys
 
 
 def kclass(name):
     if "gnca_k1_split" in name:
-        return "K1F" if ", true>" in name else "K1"
+        return "K1F" if re.search(r", (true|1|2)>", name) else "K1"
     for k in ("gnca_k2_finalize", "gnca_ks_images", "gnca_k_alive", "gnca_k0"):
         if k in name:
             return k
