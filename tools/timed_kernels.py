@@ -24,6 +24,22 @@ def kclass(name):
     return name[:40]
 
 
+def union_ms(rows):
+    """Length (ms) of the union of the rows' [start, end] intervals: with the sub-batch pipeline a
+    K1 dispatch begins when its first workgroup lands on a CU the other sub-batch's K1 has freed,
+    so one launch's begin..end includes time queued behind the other; the union is the time any K1
+    was running, the quantity the stamps measure."""
+    tot, cur = 0, None
+    for s, e in sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows):
+        if cur is None or s > cur[1]:
+            if cur:
+                tot += cur[1] - cur[0]
+            cur = [s, e]
+        else:
+            cur[1] = max(cur[1], e)
+    return (tot + (cur[1] - cur[0] if cur else 0)) / 1e6
+
+
 def main():
     trace, bench = sys.argv[1], sys.argv[2]
     out = sys.argv[3] if len(sys.argv) > 3 else None
@@ -55,9 +71,14 @@ def main():
         res["bench"] = {"ms_per_step": line["ms_per_step"], "steps": steps, "k1_ms_stamps": r["k1_ms"],
                         "kernel": r["kernel"]}
         res["device_span_ms_per_step"] = (t1 - t0) / 1e6 / steps
-        k1 = res["kernels"].get("K1F") or res["kernels"].get("K1")
-        if k1:
-            res["k1_rocprof_over_stamps"] = k1["mean_ms"] / r["k1_ms"]
+        k1n = "K1F" if "K1F" in res["kernels"] else "K1"
+        k1rows = [x for x in seg if kclass(x["Kernel_Name"]) == k1n]
+        k2rows = [x for x in seg if kclass(x["Kernel_Name"]) == "gnca_k2_finalize"]
+        if k1rows:
+            res["k1_union_ms_per_step"] = union_ms(k1rows) / steps
+            res["k2_union_ms_per_step"] = union_ms(k2rows) / steps if k2rows else 0.0
+            res["k1_k2_union_ms_per_step"] = union_ms(k1rows + k2rows) / steps
+            res["k1_union_over_stamps"] = res["k1_union_ms_per_step"] / r["k1_ms"]
     txt = json.dumps(res, indent=1)
     print(txt)
     if out:
