@@ -157,8 +157,8 @@ __host__ __device__ constexpr int ks_pstr(int rhw) {
 }
 
 struct KSLayout {
-  int xs, sp, ab, lst, cnt, cb, pg, fk, p0, p1, pbm, ft, w1, bias, w2, wm, wz, bml, total;   // byte offsets
-  int sp_slot, lst_slot;                                             // bytes per prepared-tile slot
+  int xs, sp, ab, lst, cnt, cb, fb, pg, fk, p0, p1, pbm, ft, w1, bias, w2, wm, wz, bml, total;   // byte offsets
+  int sp_slot, lst_slot, cb_slot;                                        // bytes per prepared-tile slot
 };
 
 __host__ __device__ constexpr int ks_a16(int v) { return (v + 15) & ~15; }
@@ -173,13 +173,16 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   int o = 0;
   L.sp_slot = ks_a16(RHW);
   L.lst_slot = ks_a16(TH * TW * 2);
+  L.cb_slot = ks_a16(8 * (TH * TW / 64 + 2));
   L.xs = o; o += 16 * ks_pstr(RHW) * 4;   // first: region reads fit the 16-bit DS offsets
   L.sp = o; o += 2 * L.sp_slot;           // sender plane (bytes 0/1), two slots
   L.ab = o; o += ks_a16(RHW);             // the preparer's alive bytes over the region
   L.lst = o; o += 2 * L.lst_slot;         // live-cell list (u16 cell indices), two slots
-  L.cnt = o; o += 32;                     // live cells per slot; group counter; staging-reads-done counter;
-                                          // fold: finalize-item counter, preparations done, group done-masks
-  L.cb = o; o += ks_a16(8 * (TH * TW / 64 + 2));   // the preparer's 64-cell chunk ballots
+  L.cnt = o; o += 48;                     // live cells per slot; group counter; staging-reads-done counter;
+                                          // fold: finalize-item counter, preparations done, group done-masks;
+                                          // the first tile's fire ballots done
+  L.cb = o; o += 2 * L.cb_slot;           // the preparer's 64-cell chunk keep ballots, two slots
+  L.fb = o; o += 32;                      // small tiles: the first tile's fire ballots (<= 4 chunks)
   L.pg = o; o += 2 * 16 * ((TH * TW + 31) / 32);  // per-group GroupNorm partials (fp64 pairs), two slots
   // fold (gnca_k1_split<..., FOLD>): per slot the previous step's GroupNorm constants (48 floats) and
   // the region's pre-update alive row masks P0 (one u64 per region row); the preparer's sender row
@@ -367,16 +370,30 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   int* pdone = cnt + 5;
   int fbase = 0;
   constexpr int NQB = (NQ + 63) / 64;
-  constexpr int FCH = 8, NFIT = NQB * (C / FCH);   // finalize items: 64 region quads x 8 channels
+  // 64-cell chunks of a tile; small tiles (the small-batch variants, where the first tile's preparation
+  // is on the launch's critical path): the first tile's fire ballots come from idle waves (fdone counts
+  // them), one wave per chunk
+  constexpr int NCH = (NCELL + 63) / 64;
+  constexpr bool SMALLT = NCH <= 4;
+  // finalize items: 64 region quads x FCH channels (small tiles: 4, so that a one-tile launch's
+  // items spread over the waves)
+  constexpr int FCH = SMALLT ? 4 : 8, NFIT = NQB * (C / FCH);
   // the fold reads the previous step's update field either compact (large batches) or dense NCHW
   // with the dead cells' zeros (small batches)
   constexpr bool CF = FOLD == 2;
+  static_assert(!SMALLT || 4 + NCH <= NW, "one fire wave per chunk");
+  int* fdone = cnt + 8;
+  uint64_t* fbl = reinterpret_cast<uint64_t*>(smem_b + L.fb);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   wg_stamp(a.stamps, 0);
   FPROF_DECL
-  if constexpr (FOLD) {   // the fold's counters are used before the prologue's barrier
-    if (tid == 0) { *fctr = 0; *pdone = 0; cnt[6] = 0; cnt[7] = 0; }
+  ARR_DECL
+  if constexpr (FOLD || SMALLT) {   // counters used before the prologue's barrier
+    if (tid == 0) {
+      if (FOLD) { *fctr = 0; *pdone = 0; cnt[6] = 0; cnt[7] = 0; }
+      *fdone = 0;
+    }
     __syncthreads();
   }
   if (GNCA_K1_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO);
@@ -627,13 +644,19 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
     FPROF_START();
-    while (__hip_atomic_load(pdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need_prep)
-      __builtin_amdgcn_s_sleep(1);
-    FPROF_MARK(0);
+    // the preparer's slot s (constants, P0, row tables) is read only after the wait below; an item's
+    // loads of the previous step's x (and dense dx) go out before it
+    bool prepared = false;
+    auto wait_prep = [&]() {
+      if (!prepared)
+        while (__hip_atomic_load(pdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need_prep)
+          __builtin_amdgcn_s_sleep(1);
+      if (!prepared) FPROF_MARK(0);
+      prepared = true;
+    };
     const float* fks = reinterpret_cast<const float*>(smem_b + L.fk + s * 192);
     const uint64_t* p0s = reinterpret_cast<const uint64_t*>(smem_b + L.p0 + s * ks_a16(RH * 8));
     const u32x4* fts = reinterpret_cast<const u32x4*>(smem_b + L.ft + s * FTS);
-    const float mu = fks[32], rs = fks[33], g3 = fks[34], b3 = fks[35];
     const bool gn = a.use_gn != 0;
     const float g2 = -2.f * a.gain;
     int gc0 = j0 - RX;
@@ -664,6 +687,15 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       for (int u = 0; u < FCH; ++u) xq[u] = *reinterpret_cast<const f4*>(a.xp + ((size_t)b * C + c0 + u) * HW + GNCA_FCELL);
       float dv[FCH][4];
       uint32_t bits = 15u;   // dense field: every value is used (a dead cell's is 0)
+      if constexpr (!CF) {
+#pragma unroll
+        for (int u = 0; u < FCH; ++u) {
+          const f4 d4 = *reinterpret_cast<const f4*>(a.dxp + ((size_t)b * C + c0 + u) * HW + GNCA_FCELL);
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) dv[u][kk] = d4[kk];
+        }
+      }
+      wait_prep();
       if constexpr (CF) {
         int k = gc / TW - tx0;
         k = k < 0 ? k + a.tiles_x : k;
@@ -690,14 +722,8 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
             for (int kk = 0; kk < 4; ++kk) dv[u][kk] = fb[off[kk]];
           }
         }
-      } else {
-#pragma unroll
-        for (int u = 0; u < FCH; ++u) {
-          const f4 d4 = *reinterpret_cast<const f4*>(a.dxp + ((size_t)b * C + c0 + u) * HW + GNCA_FCELL);
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) dv[u][kk] = d4[kk];
-        }
       }
+      const float mu = fks[32], rs = fks[33], g3 = fks[34], b3 = fks[35];
       if (wait_xsd) {
         const int rhi = min(RH - 1, (64 * (it / (C / FCH)) + 63) / QW);   // the item's last region row
         const uint32_t need = (uint32_t)__ballot(lane < qe && grow <= rhi);
@@ -743,17 +769,17 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   // mask (fire AND pre-alive) and live-cell list into slot `s`; the compact field's row tables and
   // the dead cells' zeros go to global memory.  The pre-update masks are the alive bytes (K2's
   // hand-over in a rollout, else gnca_k_alive over this step's alpha plane).
-  auto prep = [&](int t, int s) {
+  // pf: the fire ballots of this tile are (being) written to fbl by other waves (the first small tile)
+  auto prep = [&](int t, int s, bool pf) {
     if (GNCA_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_PREP_PRIO);
     const int b = t / a.tps, tin = t - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
-    const size_t cell0 = (size_t)i0 * W + j0;
     uint32_t* spp = reinterpret_cast<uint32_t*>(smem_b + L.sp + s * L.sp_slot);
     uint16_t* lstp = reinterpret_cast<uint16_t*>(smem_b + L.lst + s * L.lst_slot);
     uint32_t* abw = reinterpret_cast<uint32_t*>(smem_b + L.ab);
     const uint8_t* abq = reinterpret_cast<const uint8_t*>(smem_b + L.ab);
-    uint64_t* cb = reinterpret_cast<uint64_t*>(smem_b + L.cb);
+    uint64_t* cb = reinterpret_cast<uint64_t*>(smem_b + L.cb + s * L.cb_slot);
     // (1) the region's alive bytes, 4 columns per dword, all loads in flight together (fold: the
     //     masks from the finalized alpha, prep_fold)
     const uint64_t* p0q = reinterpret_cast<const uint64_t*>(smem_b + L.p0 + s * ks_a16(RH * 8));
@@ -788,12 +814,8 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // (2) keep = fire AND pre-alive per 64-cell chunk; live cells listed in cell order
-    float* outb = a.out + (size_t)b * C * HW + cell0;
     int nl = 0;
-    // small tiles (<= 4 chunks, the small-batch variants, where the first tile's prep is on the
-    // launch's critical path): every chunk's alive byte read at once and the loop unrolled
-    constexpr int NCH = (NCELL + 63) / 64;
-    constexpr bool SMALLT = NCH <= 4;
+    // small tiles: every chunk's alive byte read at once and the loop unrolled
     constexpr int CUNR = SMALLT ? 4 : 1;
     uint32_t cab[SMALLT ? NCH : 1];
     if constexpr (SMALLT && !FOLD) {
@@ -813,21 +835,22 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       bool live = false;
       const uint32_t ab_ = FOLD ? (inb ? (uint32_t)(p0q[ti + RY] >> (tj + RX + 4)) & 1u : 0u)
                                 : SMALLT ? cab[SMALLT ? (n0 >> 6) : 0] : (inb ? abq[(ti + RY) * RW + tj + RX] : 0u);
-      if (inb && (ab_ & 1u))
+      if (SMALLT && pf) {
+        if (n0 == 0)
+          while (__hip_atomic_load(fdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NCH)
+            __builtin_amdgcn_s_sleep(1);
+        live = inb && (ab_ & 1u) && ((fbl[n0 >> 6] >> lane) & 1ull);
+      } else if (inb && (ab_ & 1u)) {
         live = (GNCA_ABLATE & kAblFire) ? ((cell & 1) != 0)
                                         : fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step,
                                                   a.sample_base, b, HW, cell);
+      }
       const uint64_t bal = __ballot(live);
       const int pre = __popcll(bal & ((1ull << lane) - 1ull));
       if (lane == 0) cb[n0 >> 6] = bal;
       if (compact && inb && tj == 0) a.rpre[(size_t)t * TH + ti] = (uint32_t)(nl + pre);
-      if (live) {
-        lstp[nl + pre] = (uint16_t)n;
-      } else if (inb && !compact && !(GNCA_ABLATE & kAblZero)) {   // (compact: K2 masks by the row tables)
-        float* oz = outb + (size_t)ti * W + tj;
-#pragma unroll
-        for (int c = 0; c < C; ++c) oz[(size_t)c * HW] = 0.f;
-      }
+      if (live) lstp[nl + pre] = (uint16_t)n;
+      // (a dense field's dead cells get their zeros after the tile's groups: zero_item)
       nl += __popcll(bal);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -849,15 +872,51 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     if (GNCA_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO);
   };
 
+  // A dense update field's zeros at the dead cells of the tile at outb (slot s's keep ballots): item z
+  // = (64-cell chunk z / 4, channels 4 (z % 4) .. + 3), pulled after the tile's groups by the waves
+  // without a group (off the preparer, whose first tile is on a small launch's critical path)
+  auto zero_item = [&](int z, int s, float* outb) {
+    const uint64_t* cbs = reinterpret_cast<const uint64_t*>(smem_b + L.cb + s * L.cb_slot);
+    const int ch = z >> 2, c0 = 4 * (z & 3);
+    const int n = 64 * ch + lane;
+    const int ti = n / TW, tj = n - (n / TW) * TW;
+    if (n < NCELL && !((cbs[ch] >> lane) & 1ull)) {
+      float* oz = outb + (size_t)ti * W + tj + (size_t)c0 * HW;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) oz[(size_t)c * HW] = 0.f;
+    }
+  };
+
   PROF_DECL
   int tile = next_active(t_begin + xr_);
   // Prologue (what a small batch's launch waits out): the first tile's DMA, the preparer's planes of
   // that tile, then every weight load of this thread in flight together, then the weight images'
   // splits and LDS stores (B=8 72^2 K1: 20.0 -> 19.8 us; the preparer after the weight loads 22.3 us)
   if (!FOLD && tile < t_end) issue_dma(tile, wave, NW);
+  if constexpr (SMALLT) {   // the first tile's fire ballots, chunk wave - 4 (waves 4.. of SIMDs 0..)
+    if (wave >= 4 && wave < 4 + NCH && tile < t_end) {
+      const int b = tile / a.tps, tin = tile - b * a.tps;
+      const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+      const int n = 64 * (wave - 4) + lane;
+      const int ti = n / TW, tj = n - (n / TW) * TW;
+      const size_t cell = (size_t)(ty * TH + ti) * W + (tx * TW + tj);
+      bool f = false;
+      if (n < NCELL)
+        f = (GNCA_ABLATE & kAblFire) ? ((cell & 1) != 0)
+                                     : fire_at(a.fire_mode, a.fire, a.fire_rate, a.seed, a.rng_step, a.sample_base, b,
+                                               HW, cell);
+      const uint64_t bal = __ballot(f);
+      if (lane == 0) {
+        fbl[wave - 4] = bal;
+        __hip_atomic_fetch_add(fdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
   PROF_MARK(0);   // (prologue) first tile's DMA issue
-  if (wave == PW && tile < t_end) prep(tile, 0);
+  ARR_MARK(0);    // first DMA + fire ballots issued
+  if (wave == PW && tile < t_end) prep(tile, 0, SMALLT);
   PROF_MARK(3);   // (prologue) first tile's prep
+  ARR_MARK(1);
   float pcv = 0.f;
   if (tid < C * 27) pcv = a.perc[tid];
   if (tid == 0) { *gctr = 0; *xsd = 0; }
@@ -883,6 +942,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   if constexpr (FOLD) {   // the first tile's region: finalized by every wave (nothing to wait for)
     if (tile < t_end) finalize(tile, 0, 1, false, 0, nullptr, 0);
   }
+  ARR_MARK(2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PROF_MARK(1);   // (prologue) wait for the DMA, images and weight loads
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch; the
@@ -897,6 +957,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     if (pcv != ref) ok = 0;
   }
   const bool sobel = __syncthreads_and(ok) != 0;   // also the barrier after the images, DMA and prep
+  ARR_MARK(3);
 
   // per-lane LDS offsets of the message fragments (stacks [M0;M1], [M2;0], [M0;0], read per
   // group: kept out of the registers the group loop needs) and of the message bias of this lane's 8
@@ -931,7 +992,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const uint16_t* lst = reinterpret_cast<const uint16_t*>(smem_b + L.lst + par * L.lst_slot);
     const int nlive = cnt[par];
 
-    if (wave == PW && nxt < t_end && !(GNCA_ABLATE & kAblPrep)) prep(nxt, par ^ 1);
+    if (wave == PW && nxt < t_end && !(GNCA_ABLATE & kAblPrep)) prep(nxt, par ^ 1, false);
     PROF_MARK(3);   // preparer
 
     // ---- 32-cell groups, pulled from an LDS counter (the faster, older wave of a SIMD takes more);
@@ -1352,23 +1413,30 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       if (GNCA_K1_DYNPRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO);
     }
 
+    // then the dense field's zero items (the same counter: the waves without a group take them first)
+    const int nz = (compact || (GNCA_ABLATE & kAblZero)) ? 0 : 4 * NCH;
+    if (iter == 0) ARR_MARK(4);
+#pragma unroll 1
+    for (; q < qend + nz; q = pull()) zero_item(q - qend, par, outb);
     PROF_MARK(4);   // group loop
-    // The wave whose pull failed first (q == qend: the counter hands out consecutive values) stages
-    // the next tile as soon as every group is past its staged-plane reads, while the other waves
-    // still run their last groups' MFMAs and stores.
+    // The wave whose pull failed first (q == qend + nz: the counter hands out consecutive values)
+    // stages the next tile as soon as every group is past its staged-plane reads, while the other
+    // waves still run their last groups' MFMAs and stores.
     if constexpr (FOLD) {
       // every wave: the next tile's region finalized into the staging buffer (+ its cells into xo)
       if (nxt < t_end) finalize(nxt, par ^ 1, iter + 2, true, qend, lst, par);
-    } else if (q >= qend && q < qend + GNCA_DMA_WAVES && nxt < t_end) {
+    } else if (q >= qend + nz && q < qend + nz + GNCA_DMA_WAVES && nxt < t_end) {
       while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xbase < qend)
         __builtin_amdgcn_s_sleep(1);
-      issue_dma(nxt, q - qend, GNCA_DMA_WAVES);
+      issue_dma(nxt, q - qend - nz, GNCA_DMA_WAVES);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     PROF_MARK(0);
+    if (iter == 0) ARR_MARK(5);
     __syncthreads();   // groups done, next tile staged, pg complete, slot par^1 ready
     PROF_MARK(6);
-    gbase += qend + NW;
+    if (iter == 0) ARR_MARK(6);
+    gbase += qend + nz + NW;
     xbase += qend;
     if constexpr (FOLD) if (tid == 0) cnt[6 + par] = 0;   // this tile's group done-mask, for tile + 2
     // ---- the tile's GroupNorm partials in 8 bins (bin j: groups j, j + 8, ... in order; K2 sums the
@@ -1385,6 +1453,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   }
   PROF_STORE_W03;
   FPROF_STORE;
+  ARR_MARK(7);
   GNCA_STAMP_END(a.stamps);
 }
 

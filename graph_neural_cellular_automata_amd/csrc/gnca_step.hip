@@ -83,7 +83,14 @@ __device__ unsigned long long g_fprof[1024][32];
 #define FPROF_MARK(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); fp_acc[i] += t_ - fp_t; fp_t = t_; } while (0)
 #define FPROF_COUNT(i) do { fp_acc[i] += 1; } while (0)
 #define FPROF_STORE do { if (threadIdx.x == 0 || threadIdx.x == 192) for (int i_ = 0; i_ < 16; ++i_) g_fprof[blockIdx.x & 1023][(threadIdx.x ? 16 : 0) + i_] = fp_acc[i_]; } while (0)
+// every wave's s_memtime at up to 8 points of the split K1, relative to the wave's first instruction
+// (the critical path of a one-tile launch; gnca_arr_dump): [block][wave][point]
+__device__ unsigned long long g_arr[1024][16][8];
+#define ARR_DECL const unsigned long long arr_t0 = __builtin_amdgcn_s_memtime();
+#define ARR_MARK(k) do { if ((threadIdx.x & 63) == 0) g_arr[blockIdx.x & 1023][threadIdx.x >> 6][k] = __builtin_amdgcn_s_memtime() - arr_t0; } while (0)
 #else
+#define ARR_DECL
+#define ARR_MARK(k) do {} while (0)
 #define FPROF_DECL
 #define FPROF_START() do {} while (0)
 #define FPROF_MARK(i) do {} while (0)
@@ -2178,6 +2185,9 @@ int gnca_prof_dump(unsigned long long* out) {
 }
 int gnca_fprof_dump(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fprof), sizeof(g_fprof)) == hipSuccess ? 0 : -1;
+}
+int gnca_arr_dump(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_arr), sizeof(g_arr)) == hipSuccess ? 0 : -1;
 }
 #endif
 

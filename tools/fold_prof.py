@@ -47,6 +47,7 @@ def run():
     lib = L.load(LIB)
     lib.gnca_prof_dump.restype = ctypes.c_int
     lib.gnca_fprof_dump.restype = ctypes.c_int
+    lib.gnca_arr_dump.restype = ctypes.c_int
     dev = torch.device("cuda:0")
     wl = bench.WORKLOADS[os.environ.get("FOLDPROF_CONFIG", "headline")]
     B, H = wl["B"], wl["H"]
@@ -71,6 +72,9 @@ def run():
         fb = (ctypes.c_ulonglong * (1024 * 32))()
         assert lib.gnca_fprof_dump(fb) == 0
         ff = np.frombuffer(fb, dtype=np.uint64).reshape(1024, 32).astype(np.float64)
+        ab = (ctypes.c_ulonglong * (1024 * 16 * 8))()
+        assert lib.gnca_arr_dump(ab) == 0
+        arr = np.frombuffer(ab, dtype=np.uint64).reshape(1024, 16, 8).astype(np.float64)
         kind = "plain K1 (1-step rollout)" if steps == 1 else "fold K1 (last K1 of a 3-step rollout)"
         print(f"== {kind}: rollout {e0.elapsed_time(e1):.3f} ms (profile build), fold={S.rollout_fold(d)}")
         for title, a in (("wave 0 (SIMD 0)", full[:, :8]), ("wave 3 (preparer)", full[:, 8:])):
@@ -79,6 +83,11 @@ def run():
             print(f" {title}: mean cycles per workgroup {tot:.0f} over {len(a)} WGs")
             for i, nm in enumerate(NAMES):
                 print(f"  {nm:22s} {a[:, i].mean():12.0f} cycles  {100 * a[:, i].mean() / tot:5.1f} %")
+        used = arr[:, :, 7].sum(1) > 0
+        print(" per-wave arrival (cycles from the wave's start, mean over WGs): points = DMA+fire issued, prep done, "
+              "finalize done, past prologue barrier, groups done, zero items done (tile 0), past tile-0 barrier, end")
+        for wv in range(8):
+            print(f"  wave {wv}: " + " ".join(f"{arr[used, wv, k].mean():7.0f}" for k in range(8)))
         if steps > 1:
             for title, f in (("wave 0", ff[:, :16]), ("wave 3 (preparer)", ff[:, 16:])):
                 f = f[f.sum(1) > 0]
