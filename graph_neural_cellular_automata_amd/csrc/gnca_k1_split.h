@@ -23,9 +23,9 @@
 //   GEMM1  H[128 x 32] = W1[128 x 48] Y[48 x 32] + b1: 4 row blocks (rb) x 3 k-chunks (kc);
 //          k slot (kc, h, j) = feature kc (0 id, 1 sobel-x, 2 sobel-y) of channel 8h + j, which
 //          is exactly W1's column 16 kc + 8h + j, so lane (cell, h) computes the perception of
-//          channels 8h..8h+7 of its own cell.  Bias: one extra MFMA per rb with A = the three
-//          bias parts in k slots 0..2 of lane half 0 and B = (1, 1, 1, 0, ...) on half 0, zeros
-//          on half 1 (so b1 enters exactly, and the accumulator starts at 0).
+//          channels 8h..8h+7 of its own cell.  Bias: the accumulator starts at b1 (fp32, read
+//          from LDS; until round 4 an extra MFMA per rb over b1's three bf16 parts, which gave
+//          the same exact b1: the same bits, 4 MFMAs fewer per group).
 //   GEMM2  DL[16 x 32] = W2[16 x 128] relu(H): k-chunk s = (rb, ss) takes accumulator registers
 //          8ss..8ss+7 of H block rb as the B fragment, element j of half h = hidden row
 //          32rb + 16ss + 8(j>>2) + 4h + (j&3) (no data movement; the A image is permuted to
@@ -37,8 +37,9 @@
 //   MSG    M[16 x 32] = WM[16 x 16] G[16 x 32] (G = the gathered alive-masked x, k = channel
 //          8h + j): one k-chunk, stacks [M0;M1], [M2;0], [M0;0] (0 = a zero image), all in
 //          one accumulator: rows 0-15 + rows 16-31 = the six products.
-// Weight images (bf16, built once per persistent workgroup): W1 36 KB, bias 2 KB, W2 12 KB, WM
-// 1.5 KB + 0.5 KB of zeros; every A read is one conflict-free ds_read_b128.
+// Weight images (bf16, built once per persistent workgroup): W1 36 KB, W2 12 KB, WM 1.5 KB + 0.5 KB
+// of zeros; every A read is one conflict-free ds_read_b128.  The bias b1 is GEMM1's initial
+// accumulator in fp32 (0.5 KB, per lane half the 16 rows of its accumulator registers).
 //
 // The rest of the tile pipeline is the f32 K1's (LDS-DMA staging, alive / sender / keep planes,
 // live-cell compaction, fp64 GroupNorm partials per (tile, wave)), with 32-cell groups, byte
@@ -261,15 +262,10 @@ __device__ __forceinline__ void ks_fill_images(const K1Args& a, char* dst, int t
       st16(img + 2 * 12288, f2);
     }
   }
-  if (tid < 128) {   // bias: entry (rb, row): k slots 0..2 = the parts of b1[32rb + row]
-    uint32_t p0, p1, p2;
-    split3_pair(b1v, 0.f, p0, p1, p2);
-    u32x4 f;
-    f[0] = (p0 & 0xffffu) | (p1 << 16);
-    f[1] = p2 & 0xffffu;
-    f[2] = 0u;
-    f[3] = 0u;
-    st16(OB + tid * 16, f);
+  if (tid < 128) {   // bias: GEMM1's initial accumulator per (rb, lane half h): register r holds
+                     // b1[32rb + (r&3) + 8(r>>2) + 4h] (row = tid - 32rb)
+    const int rb = tid >> 5, row = tid & 31, hh = (row >> 2) & 1, r = (row & 3) + 4 * (row >> 3);
+    reinterpret_cast<float*>(dst + OB)[(rb * 2 + hh) * 16 + r] = b1v;
   }
   if (tid < 8 * 2 * 16) {
     u32x4 f0, f1, f2;
@@ -967,7 +963,9 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   const int wmB_o = (r32 < 16 ? L.wm + 1024 : L.wz) + ent_;
   const int wmC_o = (r32 < 16 ? L.wm : L.wz) + ent_;
   const int bml_o = L.bml + h * 32;
-  const u32x4 ones = h == 0 ? u32x4{0x3f803f80u, 0x3f80u, 0u, 0u} : u32x4{0u, 0u, 0u, 0u};
+  // GEMM1's accumulator starts at the bias (exactly the fp32 b1, as a bias MFMA over its three
+  // bf16 parts gave: one ds_read_b128 x 4 instead of an MFMA per row block)
+  auto bias_acc = [&](int rb) { return *reinterpret_cast<const f32x16*>(smem_b + L.bias + rb * 128 + h * 64); };
   // message gain: 0 for the RGBA channels (c < 4: h == 0, r < 4) under hidden_only
   const float mgain = GRAPH ? a.message_gain : 0.f;
   const bool hz = hidden_only && h == 0;
@@ -1162,7 +1160,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
           accm = mfma_bx(wmA, g1, accm);
           accm = mfma_bx(wmC, g2, accm);
         }
-        acc1[0] = mfma_bx(bz, ones, f32x16{});
+        acc1[0] = bias_acc(0);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
@@ -1194,7 +1192,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
           const u32x4 T1 = *reinterpret_cast<const u32x4*>(smem_b + w2T1 + s * 512);
           float hv[8];
           // step: ReLU of this k-chunk (+ the bias MFMA of the next row block, first chunk)
-          if (more && ss == 0) nx = mfma_bx(bz, ones, f32x16{});
+          if (more && ss == 0) nx = bias_acc(rb + 1);
 #pragma unroll
           for (int j = 0; j < 8; ++j) hv[j] = relu_nan(cur[8 * ss + j]);
           __builtin_amdgcn_sched_barrier(0);
@@ -1255,11 +1253,10 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         f32x16& ac = acc1[rb & 1];
-        const u32x4 bz = *reinterpret_cast<const u32x4*>(smem_b + L.bias + rb * 512 + r32 * 16);
         if (GNCA_ABLATE & kAblMfma) {
           ac = f32x16{};
         } else {
-          ac = mfma_bx(bz, ones, f32x16{});
+          ac = bias_acc(rb);
 #pragma unroll
           for (int kc = 0; kc < 3; ++kc) {
             const int img = L.w1 + (rb * 3 + kc) * 1024 + lane * 16;
@@ -1333,12 +1330,11 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       f32x16 acc[4];
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
-        const u32x4 bz = *reinterpret_cast<const u32x4*>(smem_b + L.bias + rb * 512 + r32 * 16);
         if (GNCA_ABLATE & kAblMfma) {
           acc[rb] = f32x16{};
           continue;
         }
-        acc[rb] = mfma_bx(bz, ones, f32x16{});
+        acc[rb] = bias_acc(rb);
 #pragma unroll
         for (int kc = 0; kc < 3; ++kc) {
           const int img = L.w1 + (rb * 3 + kc) * 1024 + lane * 16;

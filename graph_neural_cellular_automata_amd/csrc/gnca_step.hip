@@ -1206,8 +1206,13 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
 
 // one instantiation per (cell-vector width, update-field layout): each gets its own registers
 // (compact, B=1024: 75 VGPRs, 6 waves/SIMD; capping it at 64 for 8 waves measured 0.178 vs 0.163 ms)
+#ifdef GNCA_K2_MAXV   // A/B builds: a minimum of waves per SIMD (a VGPR cap), so that more K2 waves fit beside a K1
+#define GNCA_K2_ATTR __attribute__((amdgpu_waves_per_eu(GNCA_K2_MAXV)))
+#else
+#define GNCA_K2_ATTR
+#endif
 template <int V, bool COMPACT>
-__global__ __launch_bounds__(kThreads) void gnca_k2_finalize(const K2Args a) {
+__global__ __launch_bounds__(kThreads) GNCA_K2_ATTR void gnca_k2_finalize(const K2Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float sh_norm[4 + 64 + 64];
   const int tid = threadIdx.x;
