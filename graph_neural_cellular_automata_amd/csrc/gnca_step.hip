@@ -1165,9 +1165,13 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
       // the GroupNorm partials)
       typedef float vfu __attribute__((ext_vector_type(V), aligned(4)));
 #ifndef GNCA_K2_CU
-#define GNCA_K2_CU 5
+#define GNCA_K2_CU 2
 #endif
-      constexpr int CU = GNCA_K2_CU;   // channels in flight per thread (alone, B=1024 72^2: 3 0.164, 5 0.159, 8 0.183 ms)
+      // channels in flight per thread (alone, B=1024 72^2, round 3: 3 0.164, 5 0.159, 8 0.183 ms).  2:
+      // 64 VGPRs, so two K2 waves fit on a SIMD beside the 190-VGPR K1 of the sub-batch pipeline
+      // (headline step 0.5013 -> 0.4988 ms, c5 0.6495 -> 0.6478, interleaved A/B against 5 and 3:
+      // profiles/r04_ab_k2_channels.txt)
+      constexpr int CU = GNCA_K2_CU;
       for (int c0 = 0; c0 < C; c0 += CU) {
         vf xq[CU], fq[CU];
 #pragma unroll
@@ -1205,7 +1209,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
 }
 
 // one instantiation per (cell-vector width, update-field layout): each gets its own registers
-// (compact, B=1024: 75 VGPRs, 6 waves/SIMD; capping it at 64 for 8 waves measured 0.178 vs 0.163 ms)
+// (compact: 64 VGPRs with 2 channels in flight; round 3's 5 took 75 and a cap at 64 spilled)
 #ifdef GNCA_K2_MAXV   // A/B builds: a minimum of waves per SIMD (a VGPR cap), so that more K2 waves fit beside a K1
 #define GNCA_K2_ATTR __attribute__((amdgpu_waves_per_eu(GNCA_K2_MAXV)))
 #else
