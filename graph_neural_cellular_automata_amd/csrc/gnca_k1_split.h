@@ -387,7 +387,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   ARR_DECL
   if constexpr (FOLD || SMALLT) {   // counters used before the prologue's barrier
     if (tid == 0) {
-      if (FOLD) { *fctr = 0; *pdone = 0; cnt[6] = 0; cnt[7] = 0; }
+      if (FOLD) { *fctr = 0; *pdone = 0; cnt[6] = 0; cnt[7] = 0; cnt[9] = 0; cnt[10] = 0; }
       *fdone = 0;
     }
     __syncthreads();
@@ -458,7 +458,8 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   constexpr int FTS = ks_a16(PBH * 3 * 16);   // bytes per slot of the row-table copy
   static_assert(!FOLD || PBW <= 64, "one lane per column of the pooled band");
   static_assert(!FOLD || RX + 4 <= TW, "the band spans at most 3 source tile columns");
-  auto prep_fold = [&](int b, int i0, int j0, int s) {
+  // mode 0: all of it; mode 2: (d) and (e) only, after prep_fold_par's rows (the first tile)
+  auto prep_fold = [&](int b, int i0, int j0, int s, int mode) {
     float* fks = reinterpret_cast<float*>(smem_b + L.fk + s * 192);
     uint64_t* p0s = reinterpret_cast<uint64_t*>(smem_b + L.p0 + s * ks_a16(RH * 8));
     uint64_t* p1s = reinterpret_cast<uint64_t*>(smem_b + L.p1);
@@ -478,6 +479,10 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const float* xpa = a.xp + ((size_t)b * C + 3) * HW;
     const float* dpa = CF ? a.dxap + (size_t)b * HW : a.dxp + ((size_t)b * C + 3) * HW;
     FPROF_START();
+    if (mode == 2) {   // the band rows come from waves 0..3 (prep_fold_par)
+      while (__hip_atomic_load(cnt + 10, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4)
+        __builtin_amdgcn_s_sleep(1);
+    } else {
     // (a) every global load of the preparation, issued together (lanes past the band read column
     //     gcol of lane 0: valid, and masked out of the ballots)
     // (the row offset walks in a VGPR: kept per lane, the 2 x PBH row addresses would be scalar
@@ -585,6 +590,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     FPROF_MARK(6);
+    }   // mode != 2
     // (d) bit j of nf / nl: band column j is not the image's first / last column (its left / right
     // neighbour in the band is its image neighbour, not the torus wrap)
     const uint64_t nf = __ballot(lin && gcol != 0), nl = __ballot(lin && gcol != W - 1);
@@ -621,6 +627,90 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       }
     }
     FPROF_MARK(8);
+  };
+
+  // The first tile's (a) - (c) of the dense fold on waves 0..3 (one per SIMD), where a one-tile launch
+  // has nothing else to do yet: each loads and finalizes the band rows r = wave mod 4 (all loads at
+  // once); the preparer alone also sums the GroupNorm partials and publishes the constants (cnt[9]),
+  // which the others wait for; every wave counts its rows' ballots in (cnt[10]).  Same arithmetic
+  // as prep_fold: the same bits.
+  constexpr int PBR = (PBH + 3) / 4;
+  auto prep_fold_par = [&](int b, int i0, int j0) {
+    float* fks = reinterpret_cast<float*>(smem_b + L.fk);
+    uint64_t* pbm = reinterpret_cast<uint64_t*>(smem_b + L.pbm);
+    const bool gn = a.use_gn != 0;
+    const bool lin = lane < PBW;
+    int gcol = j0 - RX - 4 + (lin ? lane : 0);
+    gcol = gcol < 0 ? gcol + W : (gcol >= W ? gcol - W : gcol);
+    const float* xpa = a.xp + ((size_t)b * C + 3) * HW;
+    const float* dpa = a.dxp + ((size_t)b * C + 3) * HW;
+    int g0 = i0 - RY - 1 + wave;
+    g0 = g0 < 0 ? g0 + H : (g0 >= H ? g0 - H : g0);
+    float xv[PBR], dv[PBR];
+#pragma unroll
+    for (int k = 0; k < PBR; ++k) {
+      xv[k] = 0.f;
+      dv[k] = 0.f;
+      if (wave + 4 * k < PBH) {
+        int g = g0 + 4 * k;
+        g = g >= H ? g - H : g;
+        g = g >= H ? g - H : g;   // H may be < 8
+        xv[k] = xpa[g * W + gcol];
+        dv[k] = dpa[g * W + gcol];
+      }
+    }
+    if (wave == PW) {
+      const double* stp = a.statsp + (size_t)b * a.nst * 2;
+      double sa[4], sb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = lane + 64 * j;
+        const int tc = min(t, a.nst - 1);
+        const double pa = stp[2 * tc], pb = stp[2 * tc + 1];
+        sa[j] = t < a.nst ? pa : 0.0;
+        sb[j] = t < a.nst ? pb : 0.0;
+      }
+      const int lc = lane < C ? lane : 0;
+      const float gam_l = a.gamma ? a.gamma[lc] : 1.f, bet_l = a.beta ? a.beta[lc] : 0.f;
+      float mu = 0.f, rs = 1.f;
+      if (gn) {
+        double t1, t2;
+        wave_sum2_regs(sa, sb, &t1, &t2);
+        fin_mu_rs(t1, t2, (double)C * (double)HW, a.eps, &mu, &rs);
+      }
+      const float g3 = gn ? __shfl(gam_l, 3) : 1.f, b3 = gn ? __shfl(bet_l, 3) : 0.f;
+      if (lane < C) {
+        float sc, sh;
+        fin_consts(gn ? gam_l : 1.f, gn ? bet_l : 0.f, mu, rs, gn, &sc, &sh);
+        fks[lane] = sc;
+        fks[16 + lane] = sh;
+      }
+      if (lane == 0) {
+        fks[32] = mu;
+        fks[33] = rs;
+        fks[34] = g3;
+        fks[35] = b3;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(cnt + 9, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      while (__hip_atomic_load(cnt + 9, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    const float mu = fks[32], rs = fks[33], g3 = fks[34], b3 = fks[35];
+#pragma unroll
+    for (int k = 0; k < PBR; ++k) {
+      const int r = wave + 4 * k;
+      if (r >= PBH) continue;
+      const float xa = fin_alpha(xv[k], dv[k], mu, rs, g3, b3, a.gain, gn);
+      const uint64_t b0 = __ballot(lin && xa > a.alpha_thr), b1 = __ballot(lin && xa > a.graph_alpha_thr);
+      if (lane == 0) {
+        pbm[r] = b0;
+        pbm[PBH + r] = b1;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(cnt + 10, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
 
   // The finalize of tile t's staged region (slot s: its constants, P0 and row tables), into the
@@ -766,7 +856,8 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   // the dead cells' zeros go to global memory.  The pre-update masks are the alive bytes (K2's
   // hand-over in a rollout, else gnca_k_alive over this step's alpha plane).
   // pf: the fire ballots of this tile are (being) written to fbl by other waves (the first small tile)
-  auto prep = [&](int t, int s, bool pf) {
+  // rows_done: the fold's band rows of this tile were prepared by waves 0..3 (prep_fold_par)
+  auto prep = [&](int t, int s, bool pf, bool rows_done) {
     if (GNCA_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(GNCA_PREP_PRIO);
     const int b = t / a.tps, tin = t - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
@@ -780,7 +871,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     //     masks from the finalized alpha, prep_fold)
     const uint64_t* p0q = reinterpret_cast<const uint64_t*>(smem_b + L.p0 + s * ks_a16(RH * 8));
     if constexpr (FOLD) {
-      prep_fold(b, i0, j0, s);
+      prep_fold(b, i0, j0, s, rows_done ? 2 : 0);
     } else {
       const uint8_t* alb = a.alive + (size_t)b * HW;
       constexpr int NU = (NQA + 63) / 64;
@@ -910,7 +1001,15 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   }
   PROF_MARK(0);   // (prologue) first tile's DMA issue
   ARR_MARK(0);    // first DMA + fire ballots issued
-  if (wave == PW && tile < t_end) prep(tile, 0, SMALLT);
+  constexpr bool PAR_ROWS = FOLD && !CF;   // the dense fold (small batches): band rows on waves 0..3
+  if constexpr (PAR_ROWS) {
+    if (wave < 4 && tile < t_end) {
+      const int b = tile / a.tps, tin = tile - b * a.tps;
+      const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
+      prep_fold_par(b, ty * TH, tx * TW);
+    }
+  }
+  if (wave == PW && tile < t_end) prep(tile, 0, SMALLT, PAR_ROWS);
   PROF_MARK(3);   // (prologue) first tile's prep
   ARR_MARK(1);
   float pcv = 0.f;
@@ -990,7 +1089,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     const uint16_t* lst = reinterpret_cast<const uint16_t*>(smem_b + L.lst + par * L.lst_slot);
     const int nlive = cnt[par];
 
-    if (wave == PW && nxt < t_end && !(GNCA_ABLATE & kAblPrep)) prep(nxt, par ^ 1, false);
+    if (wave == PW && nxt < t_end && !(GNCA_ABLATE & kAblPrep)) prep(nxt, par ^ 1, false, false);
     PROF_MARK(3);   // preparer
 
     // ---- 32-cell groups, pulled from an LDS counter (the faster, older wave of a SIMD takes more);

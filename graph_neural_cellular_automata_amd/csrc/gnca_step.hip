@@ -1675,7 +1675,14 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
                (P->graph_on ? P->k == P->var->KU : P->var->KU == 0) &&
                d->alpha_thr >= 0.f && d->graph_alpha_thr >= d->alpha_thr && n < (size_t)1 << 31 &&
                P->tps * P->ppt <= 256;
+#ifdef GNCA_NO_FOLD   // A/B builds: no fold at all
+  P->fold_any = false;
+#endif
+#ifdef GNCA_FOLD_COMPACT_DEFAULT   // A/B builds: the compact fold planned by default too
+  P->fold_ok = P->fold_any;
+#else
   P->fold_ok = P->fold_any && !P->compact_ok;
+#endif
   const bool fc = P->fold_any && P->compact_ok;
   P->off_dx2 = carve(P->fold_any ? n * 4 + 256 : 0);
   P->off_stats2 = carve(P->fold_any ? (size_t)P->total_tiles * P->ppt * 2 * sizeof(double) : 0);
