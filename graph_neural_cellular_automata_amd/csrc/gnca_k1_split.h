@@ -158,7 +158,7 @@ __host__ __device__ constexpr int ks_pstr(int rhw) {
 }
 
 struct KSLayout {
-  int xs, sp, ab, lst, cnt, cb, fb, pg, fk, p0, p1, pbm, ft, w1, bias, w2, wm, wz, bml, total;   // byte offsets
+  int xs, sp, ab, lst, cnt, cb, fb, pg, fk, p0, p1, pbm, ft, w1, bias, w2, wm, wz, bml, pf, total;   // byte offsets
   int sp_slot, lst_slot, cb_slot;                                        // bytes per prepared-tile slot
 };
 
@@ -200,6 +200,7 @@ __host__ __device__ constexpr KSLayout ks_layout() {
   L.wm = o; o += 3 * 2 * 16 * 16;        // [plane][h][channel] x 16 B
   L.wz = o; o += 2 * 16 * 16;            // zeros, laid out like one WM plane
   L.bml = o; o += 2 * 8 * 4;             // message bias per (lane half h, accumulator register r)
+  L.pf = o; o += 16;                     // (images built by gnca_ks_images) perception == the Sobel bank
   L.total = o;
   return L;
 }
@@ -295,10 +296,32 @@ __device__ __forceinline__ void ks_fill_images(const K1Args& a, char* dst, int t
   if (tid < 16) reinterpret_cast<float*>(dst + OBM)[tid] = bmv;
 }
 
+// entry e (< 27) of one channel's frozen perception bank: feature e / 9 (identity, Sobel-x, Sobel-y),
+// tap e % 9 (row-major 3 x 3)
+__device__ __forceinline__ float ks_sobel_ref(int e) {
+  const int f = e / 9, tap = e % 9, tr = tap / 3, tc = tap % 3;
+  if (f == 0) return (tap == 4) ? 1.f : 0.f;
+  if (f == 1) return (float)((tc == 0 ? 1 : (tc == 2 ? -1 : 0)) * (tr == 1 ? 2 : 1));
+  return (float)((tr == 0 ? 1 : (tr == 2 ? -1 : 0)) * (tc == 1 ? 2 : 1));
+}
+
+// A workgroup barrier that orders LDS only (__syncthreads' fence also waits for every outstanding
+// global store): where nothing in the launch reads those stores back.  LDS-DMA into LDS is waited
+// for with vmcnt by its issuer.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // The weight images of a rollout, once, into global memory (K1Args::wimg); one 512-thread block.
 __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst) {
   if ((a.flags & kGraphOn) != 0) ks_fill_images<512, true, false>(a, dst, threadIdx.x);
   else ks_fill_images<512, false, false>(a, dst, threadIdx.x);
+  // are the perception weights the reference's frozen identity / Sobel bank?  (K1 reads the answer
+  // with the images instead of reducing it per launch)
+  constexpr KSLayout L = ks_layout<24, 36, 4, 4>();
+  const int tid = threadIdx.x;
+  int ok = 1;
+  if (tid < 16 * 27) ok = a.perc[tid] == ks_sobel_ref(tid % 27) ? 1 : 0;
+  const int all = __syncthreads_and(ok);
+  if (tid == 0) *reinterpret_cast<int*>(dst + (L.pf - L.w1)) = all;
 }
 
 #ifndef GNCA_FOLD_ABL
@@ -1013,19 +1036,25 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   PROF_MARK(3);   // (prologue) first tile's prep
   ARR_MARK(1);
   float pcv = 0.f;
-  if (tid < C * 27) pcv = a.perc[tid];
+  if (!a.wimg && tid < C * 27) pcv = a.perc[tid];
   if (tid == 0) { *gctr = 0; *xsd = 0; }
   if (!(GNCA_ABLATE & kAblFill)) {
     if (a.wimg) {
-      // the rollout's weight images, built once (gnca_ks_images): one LDS-DMA copy of the block
+      // the rollout's weight images, built once (gnca_ks_images): one LDS-DMA copy of the block (the
+      // fold: by waves 4.. only, each waiting for its copies before the finalize, so that no wave
+      // has to wait for its finalize's stores of x at the prologue's barrier)
       constexpr int NQI = (L.total - L.w1) / 16;
       static_assert((L.total - L.w1) % 16 == 0 && L.w1 % 16 == 0, "16-byte image block");
+      const int w0 = FOLD ? 4 : 0;
+      if (wave >= w0) {
 #pragma unroll 1
-      for (int i = wave; i < (NQI + 63) / 64; i += NW) {
-        const int q = 64 * i + lane;
-        if (q < NQI)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.wimg + 16 * q),
-                                           (__attribute__((address_space(3))) void*)(smem_b + L.w1 + 1024 * i), 16, 0, 0);
+        for (int i = wave - w0; i < (NQI + 63) / 64; i += NW - w0) {
+          const int q = 64 * i + lane;
+          if (q < NQI)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.wimg + 16 * q),
+                                             (__attribute__((address_space(3))) void*)(smem_b + L.w1 + 1024 * i), 16, 0, 0);
+        }
+        if (FOLD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     } else {
       ks_fill_images<NT, GRAPH, true>(a, smem_b + L.w1, tid);
@@ -1038,20 +1067,23 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     if (tile < t_end) finalize(tile, 0, 1, false, 0, nullptr, 0);
   }
   ARR_MARK(2);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the staging DMA and the images have landed (the fold with images: waited for above)
+  if (!(FOLD && a.wimg)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PROF_MARK(1);   // (prologue) wait for the DMA, images and weight loads
   // perception weights == the reference's frozen identity/Sobel bank? (one uniform branch; the
   // other case reads the weights from global memory, an uncommon slow path)
-  int ok = 1;
-  if (tid < C * 27) {
-    const int e = tid % 27, f = e / 9, tap = e % 9, tr = tap / 3, tc = tap % 3;
-    float ref;
-    if (f == 0) ref = (tap == 4) ? 1.f : 0.f;
-    else if (f == 1) ref = (float)((tc == 0 ? 1 : (tc == 2 ? -1 : 0)) * (tr == 1 ? 2 : 1));
-    else ref = (float)((tr == 0 ? 1 : (tr == 2 ? -1 : 0)) * (tc == 1 ? 2 : 1));
-    if (pcv != ref) ok = 0;
+  bool sobel;
+  if (a.wimg) {   // the images carry the answer (gnca_ks_images)
+    // the barrier after the images, DMA and prep: LDS only in the fold, whose finalize stores of x
+    // need not complete here (the staging DMA and the images were waited for above)
+    if (FOLD) lds_barrier();
+    else __syncthreads();
+    sobel = *reinterpret_cast<const int*>(smem_b + L.pf) != 0;
+  } else {
+    int ok = 1;
+    if (tid < C * 27 && pcv != ks_sobel_ref(tid % 27)) ok = 0;
+    sobel = __syncthreads_and(ok) != 0;   // also the barrier after the images, DMA and prep
   }
-  const bool sobel = __syncthreads_and(ok) != 0;   // also the barrier after the images, DMA and prep
   ARR_MARK(3);
 
   // per-lane LDS offsets of the message fragments (stacks [M0;M1], [M2;0], [M0;0], read per
