@@ -397,6 +397,11 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
   // finalize items: 64 region quads x FCH channels (small tiles: 4, so that a one-tile launch's
   // items spread over the waves)
   constexpr int FCH = SMALLT ? 4 : 8, NFIT = NQB * (C / FCH);
+  // the group body (GNCA_K1_LEAN): the classic small tiles take the row-block software pipeline (2),
+  // which a wave alone on its SIMD needs to overlap its MFMAs with its VALU (c2 14.0 -> 13.8 us); the
+  // graph ones would spill with it (c3 15.9 -> 16.4 us, profiles/r04_ab_small_lean2.txt), and its
+  // 250 VGPRs would leave the large tiles no room for the sub-batch pipeline's co-resident K2
+  constexpr int LEANV = (GNCA_K1_LEAN >= 1 && SMALLT && KU == 0) ? 2 : GNCA_K1_LEAN;
   // the fold reads the previous step's update field either compact (large batches) or dense NCHW
   // with the dead cells' zeros (small batches)
   constexpr bool CF = FOLD == 2;
@@ -1253,7 +1258,8 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       }
 
 #if GNCA_K1_LEAN
-#if GNCA_K1_LEAN >= 2
+      f32x16 acc2 = {};
+      if constexpr (LEANV >= 2) {
       // -- The group's GEMMs as a software pipeline over the row blocks: stage rb issues row block
       //    rb + 1's GEMM1 chain (bias + 18 products into acc1[(rb + 1) & 1]) two MFMAs at a time,
       //    each pair fenced together with one piece of row block rb's ReLU / split VALU, then rb's two
@@ -1261,7 +1267,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       //    then its ~104 split VALU with the matrix pipe idle; here the VALU sits in the MFMA shadows.
       //    The message MFMAs and GEMM1 of row block 0 carry the message tanh the same way.  Every
       //    accumulation chain keeps its order: bitwise the results of the plain body. --
-      f32x16 acc2 = {};
+      // (acc2: declared above)
       f32x16 acc1[2];
       // GEMM1 product q (0..17) of one row block: k-chunk q / 6, (A part, B part) by q % 6
       auto g1p = [&](f32x16& ac, const u32x4 (&A)[3][3], int q) {
@@ -1354,10 +1360,10 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-#else   // GNCA_K1_LEAN == 1
+      } else {   // LEANV == 1
       // -- message: M = WM.G (stacks [M0;M1] G0 + [M2;0] G0 + [M0;M1] G1 + [M0;0] G2), then the
       //    message term tanh(M + bm S) * gain seeds GEMM2's accumulator (top half; bottom 0) --
-      f32x16 acc2 = {};
+      // (acc2: declared above)
       if constexpr (GRAPH) {
         f32x16 accm = {};
         if (!(GNCA_ABLATE & kAblMfma)) {
@@ -1423,7 +1429,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         }
       }
 
-#endif   // GNCA_K1_LEAN >= 2
+      }   // LEANV
 
       // -- epilogue: dx = dl + tanh(m) * gain (already in acc2's top half) for channels
       //    c = (r&3) + 8(r>>2) + 4h; the keep mask is the live list itself --
