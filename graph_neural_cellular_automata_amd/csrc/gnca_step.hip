@@ -1215,6 +1215,9 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
 #else
 #define GNCA_K2_ATTR
 #endif
+#ifndef GNCA_K2_PRIO
+#define GNCA_K2_PRIO 3
+#endif
 template <int V, bool COMPACT>
 __global__ __launch_bounds__(kThreads) GNCA_K2_ATTR void gnca_k2_finalize(const K2Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1236,6 +1239,11 @@ __global__ __launch_bounds__(kThreads) GNCA_K2_ATTR void gnca_k2_finalize(const 
     GNCA_STAMP_END(a.stamps);
     return;
   }
+  // K2's waves issue ahead of the co-resident K1's (the sub-batch pipeline, GNCA_K1_PRIO = 2): K2 is
+  // memory-bound, so it issues its loads at once and then waits, and K1 has the SIMD meanwhile;
+  // below K1 it was starved of issue slots and held its CU share longer (headline step 0.512 ->
+  // 0.495 ms, profiles/r04_ab_k2_priority.txt)
+  __builtin_amdgcn_s_setprio(GNCA_K2_PRIO);
   k2_body<V, COMPACT>(a, smem, sh_norm);
   GNCA_STAMP_END(a.stamps);
 }
