@@ -333,11 +333,12 @@ __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst)
 #endif
 
 #ifndef GNCA_K1_PRIO
-#define GNCA_K1_PRIO 2   // wave issue priority of K1 (s_setprio): > 0 favours K1 over a co-resident K2
+#define GNCA_K1_PRIO 1   // wave issue priority of K1's groups (s_setprio): below K2's (GNCA_K2_PRIO = 3) so that a
+                         // co-resident K2 issues its loads first (round 4: 2 -> 1 with K2 at 3, step 0.4995 -> 0.4912 ms)
 #endif
 
 #ifndef GNCA_PREP_PRIO
-#define GNCA_PREP_PRIO 3   // the preparer's issue priority while it prepares (K1 0.397 -> 0.384 ms; 0: unchanged)
+#define GNCA_PREP_PRIO 2   // the preparer's issue priority while it prepares, one above the groups (K1 0.397 -> 0.384 ms; 0: unchanged)
 #endif
 
 #ifndef GNCA_K1_STAGGER
