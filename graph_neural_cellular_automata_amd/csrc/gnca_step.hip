@@ -1650,8 +1650,10 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
     // K2 bands on the compact field: ~12 rows (B=1024 72^2, tables feeding the alpha rows: 4 rows
     // 0.233, 8 0.180, 12 0.170, 24 0.170 ms; since the alpha plane is dense: 6 0.164, 8 0.158,
     // 12 0.161, 24 0.163 ms, within the box-to-box spread); wide canvases 6 rows (c5, 128^2 x 32ch,
-    // step: 4 0.662, 6 0.651, 8 0.652, 12 0.660, 16 0.657, 22 0.673 ms; tools/k2_band_c5.sh)
-    long rows = d->W >= 128 ? 6 : 12;
+    // step: 4 0.662, 6 0.651, 8 0.652, 12 0.660, 16 0.657, 22 0.673 ms; tools/k2_band_c5.sh).  Since
+    // K2 issues ahead of the co-resident K1 (round 4), 6 rows at the headline too: step 0.4920 ->
+    // 0.4865 ms over six interleaved pairs (8: 0.52, 24: 0.536; profiles/r04_k2_band_sweep.txt)
+    long rows = 6;
     static const char* band_env = GNCA_AB_ENV("GNCA_K2_BAND");   // measurement knob (A/B runs only)
     if (band_env && atoi(band_env) > 0) rows = atoi(band_env);
     const long cap = (48L * 1024 / 4 / d->W - 2) / 2;
