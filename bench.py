@@ -63,8 +63,12 @@ WORKLOADS = {
 }
 # per-launch HBM traffic of K1/K2 measured by rocprofv3 PMC counters in separate passes
 # (tools/pmc.sh + tools/pmc_traffic.py); counters cannot be read from inside this process
-PMC_TRAFFIC = max(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc_traffic.json")) or
-                  [os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")])
+# the passes of the shipped build (round 4's final tag r04h; a round's tags are not in time order, so
+# the name is explicit), else the highest-named file
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04h_pmc_traffic.json")
+if not os.path.exists(PMC_TRAFFIC):
+    PMC_TRAFFIC = max(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc_traffic.json")) or
+                      [os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")])
 
 
 def flop_per_cell(wl):
