@@ -607,6 +607,7 @@ def main():
         raise SystemExit("bench: the stamped rollout differs from the timed rollout")
     sv = stamps.view(args.steps, nsub, 2, cap, 2).cpu().numpy()
     dur = np.zeros((args.steps, nsub, 2))
+    ivs = ([], [])                      # every K1 / K2 launch's [start, end] in ticks
     first, last = None, None
     for t in range(args.steps):
         for j in range(nsub):
@@ -618,11 +619,24 @@ def main():
                     raise SystemExit(f"bench: no stamps from step {t} sub-batch {j} kernel {k}")
                 t0_, t1_ = int(sv[t, j, k, used, 0].min()), int(sv[t, j, k, used, 1].max())
                 dur[t, j, k] = (t1_ - t0_) * 1e-5          # 100 MHz ticks -> ms
+                ivs[k].append((t0_, t1_))
                 first = t0_ if first is None else min(first, t0_)
                 last = t1_ if last is None else max(last, t1_)
-    # per step: the sub-batches' launch durations summed (each sub-batch holds 1/nsub of the cells;
-    # sub-batches' K1s do not overlap each other; a K2 may overlap the other sub-batch's K1)
-    k1_ms, k2_ms = float(dur[:, :, 0].sum(1).mean()), float(dur[:, :, 1].sum(1).mean())
+    # per step: the time any K1 (K2) workgroup of the timed rollout was running, i.e. the union of the
+    # launches' intervals over the steps (each sub-batch holds 1/nsub of the cells; a sub-batch's K1
+    # starts on the CUs the other sub-batch's K1 frees, so the two launches' spans overlap and their
+    # sum would exceed the time; a K2 overlaps the other sub-batch's K1)
+    def union_ms(iv):
+        tot, cur = 0, None
+        for a_, b_ in sorted(iv):
+            if cur is None or a_ > cur[1]:
+                if cur is not None:
+                    tot += cur[1] - cur[0]
+                cur = [a_, b_]
+            else:
+                cur[1] = max(cur[1], b_)
+        return (tot + (cur[1] - cur[0] if cur is not None else 0)) * 1e-5
+    k1_ms, k2_ms = union_ms(ivs[0]) / args.steps, union_ms(ivs[1]) / args.steps
     fold_info = None
     if fold:
         # per step in steady state: the fold K1 (steps 1..K-1; step 0's K1 is the plain one, the
