@@ -116,14 +116,23 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=24.0,
                     help="wall budget of the CPU baseline (rank 0, N=1 only), split over its entries")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl (= RCCL) on a node; gloo only to rehearse N>1 ranks on one GPU")
-    ap.add_argument("--mode", default="rollout", choices=["rollout", "train"],
+    ap.add_argument("--dist-backend", default=None, choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the default for N>1) on a node; gloo only to rehearse N>1 ranks "
+                         "on one GPU.  Given explicitly at N=1, a world-1 process group of that backend "
+                         "is initialised too, so the collective code paths (the training gradient "
+                         "all-reduce) run through it")
+    ap.add_argument("--mode", default="rollout", choices=["rollout", "train", "regen"],
                     help="rollout: the BASELINE.json headline (default).  train: the graph "
-                         "trainer's BPTT iteration (SURVEY.md §8f rank 1), steps = iterations")
+                         "trainer's BPTT iteration (SURVEY.md §8f rank 1), steps = iterations.  regen: "
+                         "the regeneration diagnostic's return_attention loop (SURVEY.md §8f rank 4; "
+                         "B=1, --size canvas, steps = CA steps, one damage at step 120)")
     ap.add_argument("--train-batch", type=int, default=16, help="train: samples per GPU (config.json)")
     ap.add_argument("--train-size", type=int, default=40, help="train: canvas (config.json img_size)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    args.pg1 = args.dist_backend is not None   # N=1 with an explicit backend: a world-1 process group
+    if args.dist_backend is None:
+        args.dist_backend = "nccl"
+    return args
 
 
 def load_weights(dev, wl=None):
@@ -315,6 +324,7 @@ def main_train(args, dev, world, rank):
     # (offset draws, fire rates, short/long regime) stays in lockstep on every rank
     stab_rng = random.Random(4242 + rank)
     cells = [0]
+    ar_bytes = [0]   # bytes of the last flat gradient all-reduce (0: no process group)
     # GNCA_TRAIN_PHASES=1 (measurement only): synchronise at the phase boundaries and report the
     # mean wall time of each phase of an iteration on stderr
     phase_t = {} if os.environ.get("GNCA_TRAIN_PHASES") else None
@@ -369,7 +379,7 @@ def main_train(args, dev, world, rank):
         opt.zero_grad(set_to_none=True)
         loss.backward()
         tp = mark("backward", tp)
-        allreduce_gradients(params)
+        ar_bytes[0] = allreduce_gradients(params)
         normalize_gradients_(params)
         opt.step()
         pool.replace(idx, state.detach())
@@ -426,10 +436,77 @@ def main_train(args, dev, world, rank):
                        "parallelism": f"dp{world}"},
             "iterations_per_s": args.steps / el, "final_loss": float(loss.detach()),
             "iteration_stats": stats,
+            "backend": dist.get_backend() if dist.is_initialized() else None,
+            "allreduce_bytes": ar_bytes[0],
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def main_regen(args, dev):
+    """The regeneration diagnostic's hot loop (test_graph_augmented_regeneration.py:183-205) on one
+    GPU: per step ``state, attn = model(pre_state, fire_rate=0.5, return_attention=True)`` through
+    the module (torus mode, :125-140; the trained nca_latest.pt weights, config.json's r=4, K=8),
+    plus the loop's ``model.graph.msg_proj(pre_state)`` and its per-channel-group magnitude maps, and
+    ONE damage of the policy's square kind at step 120 (:185-189).  Timed: all --steps + 1 model
+    calls (the loop runs t = 0..steps), host offset draws and the module's launches included; the
+    PNG/MP4 writes are out of scope.  Reported as cell-updates/s = H*W*(steps+1)/time."""
+    from graph_neural_cellular_automata_amd import NeuralCAGraph
+    from graph_neural_cellular_automata_amd.damage import apply_damage_policy_
+    wl = WORKLOADS["headline"]
+    H = args.size or wl["H"]
+    torch.manual_seed(0)
+    random.seed(42)
+    model = NeuralCAGraph(16, HD, img_size=H, update_gain=GAIN, alpha_thr=THR, message_gain=MSG_GAIN,
+                          graph_d_model=D_MODEL, graph_attention_radius=wl["R"], graph_num_neighbors=wl["K"],
+                          graph_zero_padded_shift=False).to(dev).eval()
+    model.load_state_dict({k: v for k, v in load_weights(dev, wl).items()}, strict=False)
+    dmg = dict(DAMAGE_CFG, prob=1.0, kinds={"square": 1.0})
+
+    def seed():   # utils/nca_init.py:4-7 (make_seed): channels 3.. set to 1 at the centre
+        x = torch.zeros(1, 16, H, H, device=dev)
+        x[:, 3:, H // 2, H // 2] = 1.0
+        return x
+
+    def loop(steps, damage_step):
+        state = seed()
+        for t in range(steps + 1):
+            if t == damage_step:
+                apply_damage_policy_(state, dmg, epoch=999999)
+            pre_state = state.clone()
+            with torch.no_grad():
+                state, attn = model(pre_state, fire_rate=FIRE, return_attention=True)
+                M = model.graph.msg_proj(pre_state)
+                maps = (M[0, :3].abs().mean(dim=0), M[0, 3:4].abs().mean(dim=0), M[0, 4:].abs().mean(dim=0))
+        return state, attn, maps
+
+    for _ in range(max(1, args.warmup)):
+        loop(min(args.steps, 40), 20)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    state, attn, _ = loop(args.steps, 120)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    n = args.steps + 1
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    line = {
+        "metric": "cell-updates/sec of the regeneration diagnostic's return_attention loop (B=1)",
+        "value": H * H * n / el, "unit": "cell-updates/s", "n_gpus": 1, "steps": n, "warmup": args.warmup,
+        "ms_per_step": el / n * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "data": "make_seed state, trained nca_latest.pt weights (golden fixture), one square "
+                                "damage at step 120",
+        "config": {"workload": "test_graph_augmented_regeneration.py loop: model(pre_state, 0.5, "
+                               "return_attention=True) + msg_proj maps, torus r=4 K=8",
+                   "channels": 16, "hidden": HD, "height": H, "width": H, "batch_per_gpu": 1},
+        "k1": S.k1_variant(S.make_desc(
+            B=1, C=16, H=H, W=H, hidden=HD, d_model=D_MODEL, offsets=random.Random(1).sample(model.graph.offsets, wl["K"]),
+            flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE | L.ATTENTION, update_gain=GAIN,
+            alpha_thr=THR, message_gain=MSG_GAIN, fire_rate=FIRE, fire_mode=L.FIRE_RAND_F32))[0],
+        "attn_finite": bool(torch.isfinite(attn).all()), "state_finite": bool(torch.isfinite(state).all()),
+    }
+    print(json.dumps(line), flush=True)
 
 
 def launch_ranks(args) -> int:
@@ -459,8 +536,13 @@ def main():
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(1, ndev))
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or args.pg1:
         import torch.distributed as dist
+        if world == 1 and "MASTER_PORT" not in os.environ:   # no launcher: a private rendezvous
+            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+                so.bind(("127.0.0.1", 0))
+                os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(so.getsockname()[1]),
+                                  RANK="0", WORLD_SIZE="1")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -468,6 +550,8 @@ def main():
         assert dist.get_world_size() == args.gpus
     if args.mode == "train":
         return main_train(args, dev, world, rank)
+    if args.mode == "regen":
+        return main_regen(args, dev)
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
     lib = L.load()
@@ -779,7 +863,7 @@ def main():
             "config": {"workload": wl["name"], "config": args.config,
                        "channels": C, "hidden": HD, "height": H, "width": H,
                        "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}"},
-            "ranks_seen": ranks_seen, "backend": (args.dist_backend if world > 1 else None),
+            "ranks_seen": ranks_seen, "backend": (args.dist_backend if (world > 1 or args.pg1) else None),
             "rank_state_checksums": rank_sums,
             "k1_k2_ms_vs_step": (k1_ms + k2_ms) / ms,   # > 1 only where sub-batches overlap K2 with K1
             "device_timeline": {"stamped_rollout_ms_per_step": stamped_ms,
@@ -790,7 +874,7 @@ def main():
             "roofline": roof, "roofline_k2": roof_k2, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if world > 1 or args.pg1:
         dist.destroy_process_group()
 
 

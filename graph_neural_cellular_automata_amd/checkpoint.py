@@ -129,7 +129,9 @@ def load_checkpoint(payload, model, optimizer=None, scheduler=None, pool=None) -
                       f"stream", flush=True)
             else:
                 pool.set_rng_state(ranks[pool.rank])
-        else:   # a single unlabelled stream (older checkpoints): whose rank it was is unknown
-            print("[warn] checkpoint holds one unlabelled pool stream: the pool keeps its fresh "
-                  "stream", flush=True)
+        elif pool.rank == 0:   # a single unlabelled stream (older checkpoints): the saving rank's,
+            pool.set_rng_state(saved)   # which was rank 0 (the trainers save from rank 0 only)
+        else:
+            print(f"[warn] checkpoint holds one unlabelled pool stream (rank 0's): rank {pool.rank} "
+                  f"keeps its fresh stream", flush=True)
     return int(payload.get("epoch", 0)) + 1

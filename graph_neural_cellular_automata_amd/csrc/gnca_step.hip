@@ -2291,6 +2291,13 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
   const bool fold = PF.fold_ok || (PF.fold_any && (flags & GNCA_ROLLOUT_FOLD));
   const int nsub = fold ? 1 : rollout_subs(&dt);
   if ((pend_in || pend_out) && !fold) return GNCA_ERR_INVALID;
+  // an ALIVE_IN / ALIVE_OUT chain must keep one plan across its pieces: the alive masks and weight
+  // images sit at the plan's workspace offsets, and the sub-batch streams are forked by the first
+  // piece and joined by the last.  A FOLD request that changes the plan (compact field: one-stream
+  // fold instead of the sub-batch pipeline) could differ between pieces, so it is not allowed with
+  // ALIVE_*; fold chains hand over with PENDING_* instead.
+  if ((in0 || out_last) && (flags & GNCA_ROLLOUT_FOLD) && fold && !PF.fold_ok && rollout_subs(&dt) > 1)
+    return GNCA_ERR_INVALID;
   // the 16-channel split K1's weight images, once for the whole rollout (every K1 launch then copies
   // them into LDS with LDS-DMA instead of loading, splitting and storing the fp32 weights)
   const char* wimg = nullptr;

@@ -15,8 +15,10 @@ differ in length by one, and ``random.sample`` over different lengths consumes t
 differently, which would desynchronise the per-step offset draws that every rank must share
 (``sharding.py``).  That private stream is seeded from the global stream's STATE at construction
 (read, not consumed: identical on every rank, and it follows the user's ``random.seed``) mixed
-with the rank; ``rng_state()`` / ``set_rng_state()`` carry it through a checkpoint
-(``checkpoint.save_checkpoint(..., pool=)``).
+with the rank; ``rng_state()`` / ``set_rng_state()`` carry it through a checkpoint: every rank
+calls ``checkpoint.pool_rng_states(pool)`` (collective over the pool's world), rank 0 saves the
+result with ``save_checkpoint(..., pool_states=)``, and ``load_checkpoint(..., pool=)`` on each rank
+restores that rank's own stream (``save_checkpoint(..., pool=)`` stores only the calling rank's).
 """
 from __future__ import annotations
 

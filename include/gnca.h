@@ -227,7 +227,10 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
 #define GNCA_ROLLOUT_PENDING_IN  (1u << 2)
 #define GNCA_ROLLOUT_PENDING_OUT (1u << 3)
 /* Fold even on the compact update field (gnca_k1_variant arith bit 16): large batches otherwise run
- * the two-stream sub-batch pipeline, which measured faster on MI355X ("The fold"). */
+ * the two-stream sub-batch pipeline, which measured faster on MI355X ("The fold").
+ * Where the request changes the plan (it is not the default for this shape), it is GNCA_ERR_INVALID
+ * together with ALIVE_IN / ALIVE_OUT: every piece of an ALIVE chain must run one plan, and a fold
+ * chain hands over with PENDING_IN / PENDING_OUT instead. */
 #define GNCA_ROLLOUT_FOLD        (1u << 4)
 int gnca_rollout_ex_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t steps,
                         const int8_t* offsets, const float* x, float* x_final, float* scratch,

@@ -162,3 +162,52 @@ def train_rank(rank, world, port, q, policy, max_norm):
         raise
     finally:
         dist.destroy_process_group()
+
+
+# ---- RCCL on the box: a world_size-1 nccl process group ------------------------
+def nccl1_rank(rank, world, port, q):
+    """A fresh process (forkserver child: nothing here has touched the GPU before) joins a
+    world_size-1 **nccl** (= RCCL) process group and runs the trainer's flat gradient all-reduce
+    (``dp.allreduce_gradients``) on the HIP backward's gradients, plus one RCCL sum of a known
+    device tensor; the parent compares with its own un-reduced gradients."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        probe = torch.arange(1, 9, dtype=torch.float32, device=dev)
+        dist.all_reduce(probe)
+        torch.cuda.synchronize()
+        x, target = train_batch(TRAIN)
+        avg, post = train_grads(TRAIN, x, target, dev, "normalize", 0.0, True)
+        q.put({"avg": avg, "post": post, "backend": dist.get_backend(), "world": dist.get_world_size(),
+               "probe": probe.cpu().tolist()})
+    except BaseException as exc:
+        q.put({"error": f"rank {rank}: {type(exc).__name__}: {exc}"})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def bench_train_nccl(rank, world, port, q, root):
+    """``bench.py --mode train --gpus 1 --dist-backend nccl`` for a few iterations, as a child
+    process of this forkserver child (which never touches the GPU, so starting a program is safe);
+    returns bench's JSON line."""
+    import json
+    import subprocess
+    import sys
+    try:
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                   LOCAL_RANK="0")
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--mode", "train", "--gpus", "1",
+                            "--dist-backend", "nccl", "--steps", "2", "--warmup", "1"],
+                           cwd=root, env=env, capture_output=True, text=True, timeout=100)
+        if r.returncode != 0:
+            q.put({"error": f"bench rc {r.returncode}: {r.stderr[-2000:]}"})
+            return
+        q.put({"line": json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])})
+    except BaseException as exc:
+        q.put({"error": f"{type(exc).__name__}: {exc}"})
+        raise

@@ -93,3 +93,69 @@ def test_sharded_pool_streams_resume_per_rank(tmp_path):
     before = other.rng_state()
     load_checkpoint(payload, _model(), pool=other)
     assert other.rng_state() == before
+    # an older checkpoint's single unlabelled stream is the saving rank's (rank 0): restored there
+    old = dict(payload, pool_rng_state=live[0].rng_state())
+    expect0 = live[0].sample(3)[0]
+    fresh = pools(2)
+    for p in fresh:
+        load_checkpoint(old, _model(), pool=p)
+    assert fresh[0].sample(3)[0] == expect0
+    assert fresh[1].rng_state() == pools(2)[1].rng_state()
+
+
+def _pool_ckpt_rank(rank, world, port, path, q):
+    """One gloo rank of the per-rank pool-stream resume: sample, gather every rank's stream
+    (pool_rng_states, collective), rank 0 saves, every rank reloads into a fresh pool and must
+    continue its OWN sequence."""
+    import os
+    import random
+
+    import torch.distributed as dist
+
+    from graph_neural_cellular_automata_amd.checkpoint import pool_rng_states
+    from graph_neural_cellular_automata_amd.pool import SamplePool
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def seed_fn(batch_size=1):
+            return torch.zeros(batch_size, 4, 2, 2)
+
+        random.seed(5)
+        pool = SamplePool(16, seed_fn, shard=(rank, world))
+        pool.sample(3)
+        states = pool_rng_states(pool)          # collective: every rank gets the whole map
+        assert sorted(states["ranks"]) == list(range(world))
+        if rank == 0:
+            m = _model()
+            opt, sch = _opt(m)
+            save_checkpoint(path, "epoch1", m, opt, sch, epoch=1, global_step=2, pool_states=states)
+        dist.barrier()
+        expect = pool.sample(3)[0]
+        random.seed(5)
+        fresh = SamplePool(16, seed_fn, shard=(rank, world))
+        _, payload = pick_resume(path)
+        load_checkpoint(payload, _model(), pool=fresh)
+        got = fresh.sample(3)[0]
+        q.put((rank, list(expect), list(got)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pool_streams_two_rank_gloo_resume(tmp_path):
+    """the collective path of pool_rng_states end to end with two gloo ranks."""
+    import os
+
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_pool_ckpt_rank, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (e, g)) for r, e, g in (q.get(timeout=240) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        assert got[r][0] == got[r][1]        # each rank continues its own sequence
+    assert got[0][0] != got[1][0]            # and the two sequences differ

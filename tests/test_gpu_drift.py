@@ -41,7 +41,13 @@ CASES = {
     # B=16 gives 1024 tiles, above the compact field's 2-per-CU threshold on 256- and 304-CU parts
     "c5_split32": ("graph_torus_c32_r5_k16_b1_48", True, 32, 128, 16, 5, 16, 48, (0, 15),
                    "gnca_k1_split32<16,16,5,8,16>", True),
+    # zero-pad mode (the ctor default, graph_augmentation.py:85-92: rows shifted with zero fill, the
+    # column offset ignored; per-sample softmax offset weights from K0): the attention debugger's
+    # mode (test_graph_augmented_nca.py:284), on the fp32-MFMA runtime K1 that serves it
+    "graph_zeropad_f32": ("graph_zeropad_latest_grown_b1_72", True, 16, 72, 8, 4, 8, 96, (0, 7),
+                          "gnca_k1_update<16,128,0,0,0,0,0,256>", False, True),
 }
+ARITH = {"graph_zeropad_f32": "f32"}   # the others: bf16x6 (the split K1s)
 # every case's max |hip - f64| is appended here (JSON lines; the GPU box merges gpurun_out/ back)
 DRIFT_LOG = os.environ.get("GNCA_DRIFT_LOG", os.path.join(os.path.dirname(os.path.dirname(
     os.path.abspath(__file__))), "gpurun_out", "drift_log.jsonl"))
@@ -59,7 +65,8 @@ def dev():
 def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
-    fx, graph, C, H, B, R, K, T, check, k1_expected, compact = CASES[case]
+    fx, graph, C, H, B, R, K, T, check, k1_expected, compact, *rest = CASES[case]
+    zp = bool(rest and rest[0])
     c = Case(fx)
     p64 = {k: v.astype(np.float64) for k, v in c.weights.items()}
     wt = {k: torch.from_numpy(np.ascontiguousarray(v.astype(np.float32))).to(dev) for k, v in c.weights.items()}
@@ -79,18 +86,19 @@ def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
     table = O.build_offsets(R) if graph else []
     rr = random.Random(17)
     offs = [rr.sample(table, K) if graph else [] for _ in range(T)]
-    flags = L.USE_GROUPNORM | ((L.GRAPH | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE) if graph else 0)
+    flags = L.USE_GROUPNORM | ((L.GRAPH | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE) if graph else 0) | \
+        (L.ZERO_PAD_SHIFT if zp else 0)
     base = 1000
     d = S.make_desc(B=B, C=C, H=H, W=H, hidden=128, d_model=16, offsets=offs[0], flags=flags,
                     update_gain=GAIN, alpha_thr=THR, message_gain=MSG, fire_rate=FIRE,
                     fire_mode=L.FIRE_HASH, rng_seed=SEED, rng_step=0, sample_base=base)
     name, arith = S.k1_variant(d)
-    assert (name, arith) == (k1_expected, "bf16x6")
+    assert (name, arith) == (k1_expected, ARITH.get(case, "bf16x6"))
     assert S.rollout_compact(d) == compact, "the rollout's update-field layout"
     got = S.rollout(d, w, x.contiguous(), T, offs).cpu().numpy()
     assert np.isfinite(got).all()
     cfg = dict(update_gain=GAIN, alpha_thr=THR, use_groupnorm=True, graph=graph, message_gain=MSG,
-               hidden_only=True, zero_padded_shift=False, alive_to_alive=True)
+               hidden_only=True, zero_padded_shift=zp, alive_to_alive=True)
     idx = np.array(check)
     ref = x.cpu().numpy()[idx].astype(np.float64)
     for t in range(T):
@@ -101,7 +109,7 @@ def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
     print(f"[drift] {case}: {name}, {T} steps, samples {list(check)}: max |hip - f64| = {err:.3e}")
     os.makedirs(os.path.dirname(DRIFT_LOG), exist_ok=True)
     with open(DRIFT_LOG, "a") as f:
-        f.write(json.dumps({"case": case, "k1": name, "compact": compact, "fold": S.rollout_fold(d),
+        f.write(json.dumps({"case": case, "k1": name, "compact": compact, "fold": S.rollout_fold(d), "zero_pad": zp,
                             "batch": B, "canvas": H, "steps": T, "samples": list(check),
                             "max_abs_err_vs_f64": err, "mean_abs_err_vs_f64": float(np.abs(got[idx] - ref).mean()),
                             "alive_flips": flips, "tolerance": 1e-4, "time": time.time()}) + "\n")

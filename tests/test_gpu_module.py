@@ -559,6 +559,18 @@ def test_fold_rollout_pieces_bitwise(dev, B, graph):
         assert lib.gnca_rollout_ex_f32(ctypes.byref(desc(0)), ctypes.byref(w), 1, arr, x.data_ptr(),
                                        scratch.data_ptr(), torch.empty_like(x).data_ptr(), ws.data_ptr(),
                                        ws.numel(), fl, st) == -1
+    # a FOLD request that changes the plan (B=192: two sub-batch streams without it, one fold stream
+    # with it) inside an ALIVE chain: every piece of such a chain must run one plan
+    d192 = S.make_desc(B=192, C=16, H=72, W=72, hidden=128, d_model=16, offsets=offs[0], flags=flags,
+                       update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
+                       fire_mode=L.FIRE_HASH, rng_seed=11)
+    assert S.rollout_subs(d192) > 1 and not S.rollout_fold(d192) and S.rollout_fold(d192, possible=True)
+    x192 = _state(192, 16, 72, 72, dev, seed=5)
+    ws192 = S.workspace(d192, dev)
+    for fl in (L.ROLLOUT_FOLD | L.ROLLOUT_ALIVE_OUT, L.ROLLOUT_FOLD | L.ROLLOUT_ALIVE_IN):
+        assert lib.gnca_rollout_ex_f32(ctypes.byref(d192), ctypes.byref(w), 1, arr, x192.data_ptr(),
+                                       torch.empty_like(x192).data_ptr(), torch.empty_like(x192).data_ptr(),
+                                       ws192.data_ptr(), ws192.numel(), fl, st) == -1
     d8 = S.make_desc(B=8, C=16, H=40, W=40, hidden=128, d_model=16, offsets=offs[0],
                      flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
                      update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,

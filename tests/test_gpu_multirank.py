@@ -101,3 +101,55 @@ def test_c4_shard_bitwise_equals_full_pool_rollout(dev):
     shard, plan_shard = M.hip_rollout(spec, x[384:512], 384, dev)
     print(f"[multirank] plans: pool {plan_full}, shard {plan_shard}")
     assert torch.equal(full[384:512], shard)
+
+
+def _run_one(target, extra=(), timeout=110):
+    import multiprocessing as mp
+
+    assert os.environ.get("GNCA_FORKSERVER_READY") == "1", \
+        "the forkserver must start before the GPU is initialised (tests/conftest.py)"
+    ctx = mp.get_context("forkserver")
+    q = ctx.Queue()
+    port = 30500 + (os.getpid() % 500)
+    p = ctx.Process(target=target, args=(0, 1, port, q, *extra))
+    p.start()
+    try:
+        res = q.get(timeout=timeout)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert "error" not in res, res["error"]
+    assert p.exitcode == 0, p.exitcode
+    return res
+
+
+def test_rccl_world1_allreduce_of_hip_gradients(dev):
+    """RCCL's own code path on the box (device tensors, its stream ordering, a
+    world_size=1 nccl process group): the flat all-reduce of the HIP backward's gradients leaves
+    them bit for bit as the un-reduced ones of this process (train_graph_augmented_nca.py:367-375)."""
+    from tests import mr_workers as M
+    res = _run_one(M.nccl1_rank)
+    assert res["backend"] == "nccl" and res["world"] == 1
+    assert res["probe"] == [float(v) for v in range(1, 9)]
+    x, target = M.train_batch(M.TRAIN)
+    avg, post = M.train_grads(M.TRAIN, x, target, dev, "normalize", 0.0, False)
+    assert sorted(res["avg"]) == sorted(avg)
+    for k in avg:
+        assert np.array_equal(res["avg"][k], avg[k]), k
+        assert np.array_equal(res["post"][k], post[k]), k
+
+
+def test_rccl_world1_train_bench(dev):
+    """``bench.py --mode train --gpus 1 --dist-backend nccl``: the C4/C5 trainer iteration with its
+    flat gradient all-reduce through a world-1 RCCL process group."""
+    from tests import mr_workers as M
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    line = _run_one(M.bench_train_nccl, (root,), timeout=115)["line"]
+    print(f"[multirank] rccl train bench: {line['value']:.3e} cell-upd/s, backend {line['backend']}, "
+          f"all-reduce {line['allreduce_bytes']} B")
+    assert line["backend"] == "nccl" and line["n_gpus"] == 1
+    # one flat fp32 bucket of the parameters that got a gradient (<= the 10,753 trainable ones:
+    # gate_mlp never gets one)
+    assert 0 < line["allreduce_bytes"] <= 4 * 10753 and line["allreduce_bytes"] % 4 == 0
+    assert np.isfinite(line["final_loss"])
