@@ -1009,6 +1009,11 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   BPROF_STORE;
 }
 
+// BB on the split bf16 arithmetic for C = 16, hidden = 128 (A/B builds only: slower, see bwd_plan)
+#ifdef GNCA_BB_SPLIT
+#include "gnca_bb_split.h"
+#endif
+
 // ------------------------------------------------------------------------------------------
 // BC: adjoint of the perception (zero-padded 3x3 correlation) and of the gather
 // ------------------------------------------------------------------------------------------
@@ -1470,6 +1475,8 @@ static const BBVariant kBB[] = {
 struct BwdPlan {
   FwdLayout F;
   const BBVariant* bb;
+  const void* bbfn;    // the BB kernel: gnca_b_split<MSG, true> (C = 16, hidden = 128) or bb->fn
+  const void* bbfn2;   // the kernel of slices after the first (gnca_b_split<MSG, false>, or bb->fn)
   int CP, HB, nslices;
   bool graph, msg, zp, gn;
   int RY, RX;
@@ -1551,8 +1558,52 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
       }
   }
   if (!P->bb) return false;
+  P->bbfn = P->bbfn2 = P->bb->fn;
+  // C = 16, hidden = 128: the split-arithmetic BB (gnca_bb_split.h), two 64-unit hidden slices (the
+  // per-wave weight-gradient accumulators of the whole hidden layer do not fit the register file),
+  // its own tile (the cheapest by the same makespan model within its LDS: weight images 28 KB + 4 x
+  // 16 KB wave scratch)
+  // Measured slower than the fp32-MFMA gnca_b_mlp at B=1024 72^2 (4.09 vs 3.24 ms for BB: stores of
+  // dY / dG and the per-tile staging stall its one wave per SIMD), so it is built only
+  // in A/B builds (-DGNCA_BB_SPLIT); the product backward runs gnca_b_mlp.
+#ifdef GNCA_BB_SPLIT
+  const bool split_bb = C == 16 && Hd == 128;
+  if (split_bb) {
+    double bestS = 1e300;
+    int sth = 0, stw = 0;
+    size_t slds = 0;
+    for (int th : ths)
+      for (int tw : tws) {
+        if ((th * tw) % 64 || tw + 2 * rx + 2 > 64) continue;
+        if (eth && (th != eth || tw != etw)) continue;
+        const BSLayout L = bs_layout(th, tw, ry, rx);
+        // + the kernel's static LDS (offset weights) and a margin
+        if ((size_t)L.total + GNCA_MAX_OFFSETS * 4 + 256 > 160 * 1024) continue;
+        const long tx = (W + tw - 1) / tw, ty = (H + th - 1) / th;
+        const long tiles = (long)d->B * tx * ty, cus = bwd_device_cus();
+        const long rounds = (tiles + cus - 1) / cus;
+        // per tile: its cells (in 32-cell groups) + the staged halo + a fixed part
+        const double per_tile = (double)th * tw + 0.01 * L.RH * L.RW * 16 + 60.0;
+        const double cost = (double)std::max<long>(rounds * cus, tiles) * per_tile;
+        if (cost < bestS) { bestS = cost; sth = th; stw = tw; slds = (size_t)L.total; }
+      }
+    if (sth) {
+      P->TH = sth;
+      P->TW = stw;
+      P->ldsB = slds;
+      P->bbfn = P->msg ? reinterpret_cast<const void*>(&gnca_b_split<true, true>)
+                       : reinterpret_cast<const void*>(&gnca_b_split<false, true>);
+      P->bbfn2 = P->msg ? reinterpret_cast<const void*>(&gnca_b_split<true, false>)
+                        : reinterpret_cast<const void*>(&gnca_b_split<false, false>);
+      P->HB = kBSHB;
+      P->nslices = 128 / kBSHB;
+    }
+  }
+#endif
+  if (P->bbfn == P->bb->fn) {
   P->HB = P->bb->HB;
   P->nslices = (Hd + P->HB - 1) / P->HB;
+  }
   P->tiles_x = (W + P->TW - 1) / P->TW;
   P->tps = P->tiles_x * ((H + P->TH - 1) / P->TH);
   P->total_tiles = P->tps * d->B;
@@ -1757,12 +1808,13 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     if (P.gn) a.flags |= kGN;
     const int RW = P.TW + 2 * P.RX;
     for (int o = 0; o < a.k; ++o) a.odl[o] = d.offsets[2 * o] * RW + (P.zp ? 0 : d.offsets[2 * o + 1]);
-    (void)hipFuncSetAttribute(P.bb->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.ldsB);
+    (void)hipFuncSetAttribute(P.bbfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.ldsB);
+    (void)hipFuncSetAttribute(P.bbfn2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.ldsB);
     for (int s = 0; s < P.nslices; ++s) {
       a.h0 = s * P.HB;
       a.flags = (a.flags & ~kFirst) | (s == 0 ? kFirst : 0u);
       void* args[] = {&a};
-      const hipError_t e = hipLaunchKernel(P.bb->fn, dim3(P.gridB), dim3(kThreads), args, P.ldsB, st);
+      const hipError_t e = hipLaunchKernel(s == 0 ? P.bbfn : P.bbfn2, dim3(P.gridB), dim3(kThreads), args, P.ldsB, st);
       if (e != hipSuccess) { g_last_hip = (int)e; return GNCA_ERR_HIP; }
       if ((rc = bwd_check()) != GNCA_OK) return rc;
     }

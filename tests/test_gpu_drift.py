@@ -115,3 +115,59 @@ def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
                             "alive_flips": flips, "tolerance": 1e-4, "time": time.time()}) + "\n")
     assert err <= 1e-4, err
     np.testing.assert_array_equal(O.alive_mask(got[idx], THR), O.alive_mask(ref, THR))
+
+
+@pytest.mark.parametrize("zp", [False, True])
+def test_attention_rollout_drift_vs_f64_oracle(dev, zp):
+    """The diagnostics' loops at the headline canvas: one step per call with
+    ``return_attention`` (torus: the regeneration diagnostic, test_graph_augmented_regeneration.py:194;
+    zero-pad: the attention debugger, test_graph_augmented_nca.py:284-307), 64 steps of B=2 x 72^2 on
+    the trained nca_latest.pt weights, the hashed fire mask per step: the state after every step and
+    the final step's attention map against the float64 oracle (state atol 1e-4 and no alive flips;
+    the min-max normalised map atol 1e-4)."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    c = Case("graph_torus_latest_grown_b1_72")
+    p64 = {k: v.astype(np.float64) for k, v in c.weights.items()}
+    wt = {k: torch.from_numpy(np.ascontiguousarray(v.astype(np.float32))).to(dev) for k, v in c.weights.items()}
+    w, keep = S.make_weights(dict(
+        perception=wt["perception.conv.weight"], w1=wt["update_net.0.weight"], b1=wt["update_net.0.bias"],
+        w2=wt["update_net.2.weight"], gn_weight=wt["norm.weight"], gn_bias=wt["norm.bias"],
+        wq=wt["graph.query_proj.weight"], bq=wt["graph.query_proj.bias"], wk=wt["graph.key_proj.weight"],
+        bk=wt["graph.key_proj.bias"], wm=wt["graph.msg_proj.weight"], bm=wt["graph.msg_proj.bias"],
+        scaling=wt["graph.scaling"]))
+    B, H, T = 2, 72, 64
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.rand(B, 16, H, H, device=dev, generator=g)
+    x[:, 4:] = torch.randn(B, 12, H, H, device=dev, generator=g)
+    table = O.build_offsets(4)
+    rr = random.Random(29)
+    offs = [rr.sample(table, 8) for _ in range(T)]
+    flags = L.USE_GROUPNORM | L.GRAPH | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE | L.ATTENTION | \
+        (L.ZERO_PAD_SHIFT if zp else 0)
+    cfg = dict(update_gain=GAIN, alpha_thr=THR, use_groupnorm=True, graph=True, message_gain=MSG,
+               hidden_only=True, zero_padded_shift=zp, alive_to_alive=True)
+    ref = x.cpu().numpy().astype(np.float64)
+    cur = x
+    for t in range(T):
+        d = S.make_desc(B=B, C=16, H=H, W=H, hidden=128, d_model=16, offsets=offs[t], flags=flags,
+                        update_gain=GAIN, alpha_thr=THR, message_gain=MSG, fire_rate=FIRE,
+                        fire_mode=L.FIRE_HASH, rng_seed=SEED, rng_step=t, sample_base=0)
+        cur, attn = S.step(d, w, cur, want_attention=True)
+        fm = O.hash_fire_mask(SEED, t, 0, B, H, H, FIRE)
+        ref, ref_attn = O.nca_step(ref, p64, cfg, chosen=offs[t], fire_mask=fm, return_attention=True)
+    got = cur.cpu().numpy()
+    err = float(np.abs(got - ref).max())
+    aerr = float(np.abs(attn.cpu().numpy() - ref_attn).max())
+    flips = int((O.alive_mask(got, THR) != O.alive_mask(ref, THR)).sum())
+    name, _ = S.k1_variant(d)
+    print(f"[drift] attention {'zero-pad' if zp else 'torus'}: {name}, {T} steps: max |hip - f64| = {err:.3e}, "
+          f"attention map {aerr:.3e}, alive flips {flips}")
+    os.makedirs(os.path.dirname(DRIFT_LOG), exist_ok=True)
+    with open(DRIFT_LOG, "a") as f:
+        f.write(json.dumps({"case": "attention_" + ("zeropad" if zp else "torus"), "k1": name, "zero_pad": zp,
+                            "batch": B, "canvas": H, "steps": T, "max_abs_err_vs_f64": err,
+                            "attention_max_abs_err": aerr, "alive_flips": flips, "tolerance": 1e-4,
+                            "time": time.time()}) + "\n")
+    assert err <= 1e-4 and aerr <= 1e-4, (err, aerr)
+    assert flips == 0
