@@ -965,7 +965,14 @@ __device__ __forceinline__ int k2_sample(int j, int B, int zigzag) {
 // is issued before the first barrier: a small-batch launch waits out one memory latency, not
 // one per phase.
 
-template <int V, bool COMPACT>
+#ifndef GNCA_K2_CU
+#define GNCA_K2_CU 2
+#endif
+#ifndef GNCA_K2_CU_ALONE
+#define GNCA_K2_CU_ALONE 2
+#endif
+// CU: channels in flight per thread of the compact field's main pass (below)
+template <int V, bool COMPACT, int CU>
 __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_norm) {
   typedef float vf __attribute__((ext_vector_type(V)));
 #ifndef GNCA_K2_KU
@@ -1164,14 +1171,12 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
       // to V-1 floats past the live ones stays inside the workspace: the dx field is followed by
       // the GroupNorm partials)
       typedef float vfu __attribute__((ext_vector_type(V), aligned(4)));
-#ifndef GNCA_K2_CU
-#define GNCA_K2_CU 2
-#endif
-      // channels in flight per thread (alone, B=1024 72^2, round 3: 3 0.164, 5 0.159, 8 0.183 ms).  2:
-      // 64 VGPRs, so two K2 waves fit on a SIMD beside the 190-VGPR K1 of the sub-batch pipeline
-      // (headline step 0.5013 -> 0.4988 ms, c5 0.6495 -> 0.6478, interleaved A/B against 5 and 3:
-      // profiles/r04_ab_k2_channels.txt)
-      constexpr int CU = GNCA_K2_CU;
+      // channels in flight per thread: beside the other sub-batch's K1 (the sub-batch pipeline) 2
+      // (GNCA_K2_CU: 64 VGPRs, so two K2 waves fit on a SIMD beside the 190-VGPR K1; headline step
+      // 0.5013 -> 0.4988 ms, c5 0.6495 -> 0.6478, interleaved A/B against 5 and 3:
+      // profiles/r04_ab_k2_channels.txt); alone on the chip (one-stream rollouts such as C4's 128-sample
+      // shard, the fold's last K2) also 2 (GNCA_K2_CU_ALONE, an A/B knob: round 5, interleaved, 5 vs 2 at
+      // C4's shard B=128 72^2 0.0832 vs 0.0822 ms/step, c5 0.654 vs 0.653; profiles/r05f_ab_k2_alone.txt)
       for (int c0 = 0; c0 < C; c0 += CU) {
         vf xq[CU], fq[CU];
 #pragma unroll
@@ -1218,7 +1223,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
 #ifndef GNCA_K2_PRIO
 #define GNCA_K2_PRIO 3
 #endif
-template <int V, bool COMPACT>
+template <int V, bool COMPACT, int CU = GNCA_K2_CU>
 __global__ __launch_bounds__(kThreads) GNCA_K2_ATTR void gnca_k2_finalize(const K2Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float sh_norm[4 + 64 + 64];
@@ -1244,7 +1249,7 @@ __global__ __launch_bounds__(kThreads) GNCA_K2_ATTR void gnca_k2_finalize(const 
   // below K1 it was starved of issue slots and held its CU share longer (headline step 0.512 ->
   // 0.495 ms, profiles/r04_ab_k2_priority.txt)
   __builtin_amdgcn_s_setprio(GNCA_K2_PRIO);
-  k2_body<V, COMPACT>(a, smem, sh_norm);
+  k2_body<V, COMPACT, CU>(a, smem, sh_norm);
   GNCA_STAMP_END(a.stamps);
 }
 
@@ -1869,7 +1874,9 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
                      const void* fire, float* attn, void* ws, size_t ws_bytes, hipStream_t st,
                      uint32_t phases = GNCA_PHASE_ALL, const uint8_t* active = nullptr,
                      bool alive_in = false, bool alive_out = false, bool compact = false,
-                     uint64_t* stamps = nullptr, int stamp_cap = 0, const char* wimg = nullptr, int set = 0) {
+                     uint64_t* stamps = nullptr, int stamp_cap = 0, const char* wimg = nullptr, int set = 0,
+                     bool k2_co = false) {
+  // k2_co: this step's K2 runs beside another sub-batch stream's K1 (the rollout's sub-batch pipeline)
   Plan P;
   if (!make_plan(d, false, &P)) {
     if (d && d->C >= 4 && d->hidden > 0 && !find_variant(d->C, d->hidden)) return GNCA_ERR_UNSUPPORTED;
@@ -1961,7 +1968,9 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
     if ((compact ? P.total2_c : P.total2) > stamp_cap) return GNCA_ERR_INVALID;
     k2.stamps = stamps + 2 * (size_t)stamp_cap;
   }
-  auto k2fn = compact ? ((d->W & 3) == 0 ? gnca_k2_finalize<4, true> : gnca_k2_finalize<1, true>)
+  auto k2fn = compact ? (k2_co ? ((d->W & 3) == 0 ? gnca_k2_finalize<4, true> : gnca_k2_finalize<1, true>)
+                              : ((d->W & 3) == 0 ? gnca_k2_finalize<4, true, GNCA_K2_CU_ALONE>
+                                                 : gnca_k2_finalize<1, true, GNCA_K2_CU_ALONE>))
                       : ((d->W & 3) == 0 ? gnca_k2_finalize<4, false> : gnca_k2_finalize<1, false>);
   hipLaunchKernelGGL(k2fn, dim3(compact ? P.total2_c : P.total2), dim3(kThreads),
                      compact ? P.lds2_c : P.lds2, st, k2);
@@ -2409,7 +2418,7 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
       rc = step_impl(&sd[j], w, src + elem0[j], dst + elem0[j], nullptr, nullptr, wsb + off[j], wsz[j], sj[j],
                      GNCA_PHASE_ALL, nullptr, hand_alive && (t > 0 || in0),
                      hand_alive && (t + 1 < steps || out_last), true,
-                     stamps ? stamps + ((size_t)t * nsub + j) * 4 * stamp_cap : nullptr, stamp_cap, wimg);
+                     stamps ? stamps + ((size_t)t * nsub + j) * 4 * stamp_cap : nullptr, stamp_cap, wimg, 0, true);
     }
   }
   // join (also after a failed launch: the helper streams' work stays ordered before the caller's);
