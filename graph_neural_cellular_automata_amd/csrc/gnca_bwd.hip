@@ -50,6 +50,7 @@ __device__ float g_bzero[4];   // LDS-DMA source for off-image cells (zero-initi
 constexpr uint32_t kMsg = 1u << 16;      // message path active (k > 0 and message_gain != 0)
 constexpr uint32_t kFirst = 1u << 17;    // first hidden slice: also the message backward
 constexpr uint32_t kGN = 1u << 18;       // GroupNorm on
+constexpr uint32_t kZeroed = 1u << 19;   // dY / dG / dmb were zero-filled before BB: no dead-cell zero stores
 
 // Measurement-only phase timers of BB (tools/bprof.py builds with -DGNCA_PROFILE): wave 0 of each
 // workgroup accumulates s_memtime deltas per phase; gnca_bprof_dump copies them out.
@@ -544,7 +545,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     __syncthreads();
     BPROF_MARK(7);   // loop tail
     if (a.active && !a.active[b]) {   // masked step, inactive sample: every cell is dead
-      if (first)
+      if (first && !(a.flags & kZeroed))
         for (int n = tid; n < ncell; n += kThreads) {
           const int ti = n / TW, tj = n - (n / TW) * TW;
           if (i0 + ti >= H || j0 + tj >= W) continue;
@@ -671,7 +672,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       }
       if (live) {
         lst[off + pre] = n;
-      } else if (inb && first) {
+      } else if (inb && first && !(a.flags & kZeroed)) {
         const int ce = (i0 + ti) * W + (j0 + tj);
         for (int pl = 0; pl < 3 * C; ++pl) dYb[pl * HWi + ce] = 0.f;
         if (msg)
@@ -1806,6 +1807,17 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     a.flags = d.flags & (GNCA_ZERO_PAD_SHIFT | GNCA_ALIVE_TO_ALIVE | GNCA_HIDDEN_ONLY);
     if (P.msg) a.flags |= kMsg;
     if (P.gn) a.flags |= kGN;
+#ifdef GNCA_BB_MEMSET
+    // A/B builds: the dead cells' dY / dG / <dm, b_M> zeros as one streaming fill of the three
+    // buffers ahead of BB instead of BB's per-dead-cell stores.  Measured slower (B=1024 72^2 bwd
+    // 4.77-4.79 vs 4.75-4.76 ms, B=16 40^2 0.100 vs 0.097 ms): the fill writes every cell, the live
+    // ones twice, while the dead-cell stores overlap BB's MFMA work
+    if (hipMemsetAsync(dY, 0, 3 * (size_t)B * C * HW * sizeof(float), st) != hipSuccess ||
+        (P.msg && hipMemsetAsync(dG, 0, (size_t)B * C * HW * sizeof(float), st) != hipSuccess) ||
+        (dmb && hipMemsetAsync(dmb, 0, (size_t)B * HW * sizeof(float), st) != hipSuccess))
+      return GNCA_ERR_HIP;
+    a.flags |= kZeroed;
+#endif
     const int RW = P.TW + 2 * P.RX;
     for (int o = 0; o < a.k; ++o) a.odl[o] = d.offsets[2 * o] * RW + (P.zp ? 0 : d.offsets[2 * o + 1]);
     (void)hipFuncSetAttribute(P.bbfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.ldsB);

@@ -2063,14 +2063,20 @@ static void sub_desc(const gnca_step_desc* d, int sub, int nsub, gnca_step_desc*
 static int rollout_subs(const gnca_step_desc* d) {
   if (kRolloutSubs < 2 || !d || d->B < kRolloutSubs) return 1;
   Plan P;
+#ifdef GNCA_SUBS_ANY   // A/B builds: the 32-channel K1 too (it leaves no room for a co-resident K2)
+  if (!make_plan(d, false, &P) || P.var->split == 0 || !P.compact_ok || P.fold_ok) return 1;
+#else
   if (!make_plan(d, false, &P) || P.var->split != 1 || !P.compact_ok || P.fold_ok) return 1;   // (fold_ok: dense)
+#endif
   for (int s = 0; s < kRolloutSubs; ++s) {
     gnca_step_desc sd;
     int b0;
     sub_desc(d, s, kRolloutSubs, &sd, &b0);
     Plan Q;
     if (!make_plan(&sd, false, &Q) || Q.var != P.var || !Q.compact_ok) return 1;
+#ifndef GNCA_SUBS_ANY
     if (Q.lds1 + Q.lds2_c + 512 > (size_t)max_lds_bytes()) return 1;   // K2's static LDS + margin
+#endif
   }
   return kRolloutSubs;
 }
