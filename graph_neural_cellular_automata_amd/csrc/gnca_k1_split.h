@@ -355,8 +355,18 @@ __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst)
 
 // FOLD: 0 = the plain K1; 1 / 2 = the fold variant (this launch also finishes the previous step,
 // below) on the previous step's dense / compact update field
+#ifdef GNCA_K1_MAXVGPR   // A/B builds: a VGPR cap below the occupancy's (room for a co-resident K2 wave)
+#define GNCA_K1_VATTR __attribute__((amdgpu_num_vgpr(GNCA_K1_MAXVGPR)))
+#else
+#define GNCA_K1_VATTR
+#endif
+
+#ifndef GNCA_K1_LB
+#define GNCA_K1_LB GNCA_K1_SPLIT_NT   // A/B builds: launch bounds above the launched size (a VGPR cap)
+#endif
+
 template <int TH, int TW, int RY, int RX, int KU, int FOLD = 0>
-__global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Args a) {
+__global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_b[];
   constexpr int C = 16, HD = 128, NT = GNCA_K1_SPLIT_NT, NW = NT / 64;
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
@@ -516,6 +526,21 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     //     gcol of lane 0: valid, and masked out of the ballots)
     // (the row offset walks in a VGPR: kept per lane, the 2 x PBH row addresses would be scalar
     //  pairs and spill)
+#ifdef GNCA_FOLD_PROTO_ALIVE   // timing-only prototype: the band's masks as bytes from memory (wrong results)
+    uint32_t xv[PBH];
+    {
+      int g0 = i0 - RY - 1;
+      g0 = g0 < 0 ? g0 + H : g0;
+      uint32_t off = (uint32_t)(g0 * W + gcol);
+      const uint8_t* alb = a.alive + (size_t)b * HW;
+#pragma unroll
+      for (int r = 0; r < PBH; ++r) {
+        xv[r] = alb[off];
+        off += (uint32_t)W;
+        off = off >= (uint32_t)HW ? off - (uint32_t)HW : off;
+      }
+    }
+#else
     float xv[PBH], dv[PBH];
     {
       int g0 = i0 - RY - 1;
@@ -529,6 +554,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         off = off >= (uint32_t)HW ? off - (uint32_t)HW : off;   // the torus wrap of the next row
       }
     }
+#endif
     constexpr int NFT = PBH * 3, NFTU = (NFT + 63) / 64;
     uint64_t fm[NFTU];
     uint32_t fp[NFTU], ft_[NFTU];
@@ -596,6 +622,12 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     FPROF_MARK(5);
     // (c) the finalized alpha's threshold bits, one ballot pair per band row
     // (the compact field's live bits of this lane's column, all rows read from the slot first)
+#ifdef GNCA_FOLD_PROTO_ALIVE
+    (void)kcol; (void)tjS; (void)xpa; (void)dpa;
+#pragma unroll
+    for (int r = 0; r < PBH; ++r) {
+      const uint64_t b0 = __ballot(lin && (xv[r] & 1u)), b1 = __ballot(lin && (xv[r] & 2u));
+#else
     uint32_t lv[PBH];
 #pragma unroll
     for (int r = 0; r < PBH; ++r) {
@@ -610,6 +642,7 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
     for (int r = 0; r < PBH; ++r) {
       const float xa = xv[r];
       const uint64_t b0 = __ballot(lin && xa > a.alpha_thr), b1 = __ballot(lin && xa > a.graph_alpha_thr);
+#endif
       if (lane == 0) {   // stored right away: no scalar pair stays live past its row
         pbm[r] = b0;
         pbm[PBH + r] = b1;
@@ -1153,6 +1186,8 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       const int hb = 8 * h * PSTR;          // this lane's channel half
       const int relcell = ti * W + tj;
 
+      // GEMM2's accumulator (the lean bodies: seeded with the message term)
+      f32x16 acc2 = {};
       // -- gather of alive-masked x, channels 8h..8h+7 (uniform weight 1/k, applied once) --
       u32x4 g0 = {0u, 0u, 0u, 0u}, g1 = g0, g2 = g0;
       float S = 0.f;
@@ -1190,6 +1225,26 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
         asm volatile("" : "+v"(g0), "+v"(g1), "+v"(g2), "+v"(S));
       }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (GRAPH && LEANV == 3) {
+        // the message right after the gather (its operands die before the perception's live):
+        // M = WM.G, then tanh(M + bm S) * gain seeds GEMM2's accumulator (top half; bottom 0)
+        f32x16 accm = {};
+        if (!(GNCA_ABLATE & kAblMfma)) {
+          const u32x4 wmA = *reinterpret_cast<const u32x4*>(smem_b + wmA_o);
+          accm = mfma_bx(wmA, g0, accm);
+          const u32x4 wmB = *reinterpret_cast<const u32x4*>(smem_b + wmB_o);
+          accm = mfma_bx(wmB, g0, accm);
+          accm = mfma_bx(wmA, g1, accm);
+          const u32x4 wmC = *reinterpret_cast<const u32x4*>(smem_b + wmC_o);
+          accm = mfma_bx(wmC, g2, accm);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float bm_ = reinterpret_cast<const float*>(smem_b + bml_o)[r];
+          acc2[r] = fast_tanh(fmaf(bm_, S, accm[r] + accm[r + 8])) * ((hz && r < 4) ? 0.f : mgain);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
 
       // -- perception of channels 8h..8h+7 (zero padding at the image border via zero taps) --
       float y0[8], y1[8], y2[8];
@@ -1259,8 +1314,55 @@ __global__ __launch_bounds__(GNCA_K1_SPLIT_NT, 1) void gnca_k1_split(const K1Arg
       }
 
 #if GNCA_K1_LEAN
-      f32x16 acc2 = {};
-      if constexpr (LEANV >= 2) {
+      if constexpr (LEANV == 3) {
+      // -- GEMM1 row block rb into ONE accumulator, then its ReLU / split and its two GEMM2 k-chunks,
+      //    the row blocks strictly one after another (fenced): the fewest registers live, so that
+      //    three K1 waves share a SIMD (768 threads) and the other waves hide each chain's latency.
+      //    Same products in the same order as the other bodies: the same bits. --
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          f32x16 ac;
+          if (GNCA_ABLATE & kAblMfma) {
+            ac = f32x16{};
+          } else {
+            ac = bias_acc(rb);
+#pragma unroll
+            for (int kc = 0; kc < 3; ++kc) {
+              const int img = L.w1 + (rb * 3 + kc) * 1024 + lane * 16;
+              const u32x4 a0 = *reinterpret_cast<const u32x4*>(smem_b + img);
+              const u32x4 a1 = *reinterpret_cast<const u32x4*>(smem_b + img + 12288);
+              const u32x4 a2 = *reinterpret_cast<const u32x4*>(smem_b + img + 24576);
+              ac = mfma_bx(a0, yf[kc][0], ac);
+              ac = mfma_bx(a0, yf[kc][1], ac);
+              ac = mfma_bx(a1, yf[kc][0], ac);
+              ac = mfma_bx(a0, yf[kc][2], ac);
+              ac = mfma_bx(a2, yf[kc][0], ac);
+              ac = mfma_bx(a1, yf[kc][1], ac);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+#pragma unroll
+          for (int ss = 0; ss < 2; ++ss) {
+            const int s = 2 * rb + ss;
+            float hv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) hv[j] = relu_nan(ac[8 * ss + j]);
+            u32x4 h0, h1, h2;
+            split3_x8(hv, h0, h1, h2);
+            if (GNCA_ABLATE & kAblMfma) {
+              asm volatile("" ::"v"(h0), "v"(h1), "v"(h2));
+              continue;
+            }
+            const u32x4 T0 = *reinterpret_cast<const u32x4*>(smem_b + w2T0 + s * 512);
+            const u32x4 T1 = *reinterpret_cast<const u32x4*>(smem_b + w2T1 + s * 512);
+            acc2 = mfma_bx(T0, h0, acc2);
+            acc2 = mfma_bx(T1, h0, acc2);
+            acc2 = mfma_bx(T0, h1, acc2);
+            acc2 = mfma_bx(T0, h2, acc2);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      } else if constexpr (LEANV >= 2) {
       // -- The group's GEMMs as a software pipeline over the row blocks: stage rb issues row block
       //    rb + 1's GEMM1 chain (bias + 18 products into acc1[(rb + 1) & 1]) two MFMAs at a time,
       //    each pair fenced together with one piece of row block rb's ReLU / split VALU, then rb's two

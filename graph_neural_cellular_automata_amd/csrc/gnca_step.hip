@@ -1829,6 +1829,9 @@ static int launch_k0(const gnca_step_desc* d, const gnca_weights* w, const Plan&
 static int launch_k1(const K1Args& k1, const Plan& P, hipStream_t st) {
   const int occ = occupancy(P.var->fn, P.lds1, P.var->NT);
   long grid = (long)device_cus() * occ;
+  // measurement knob (A/B builds only): leave CUs free of K1 workgroups (for K2 of the other sub-batch)
+  static const char* free_env = GNCA_AB_ENV("GNCA_K1_FREE_CUS");
+  if (free_env) grid -= atoi(free_env);
   if (grid > P.total_tiles) grid = P.total_tiles;
   if (grid < 1) grid = 1;
   void* args[] = {const_cast<K1Args*>(&k1)};
@@ -2006,6 +2009,9 @@ static int fold_k1(const gnca_step_desc* d, const gnca_weights* w, const Plan& P
   k1.nst = P.tps * P.ppt;
   k1.wimg = wimg;
   k1.stamps = stamps;
+#ifdef GNCA_FOLD_PROTO_ALIVE
+  k1.alive = reinterpret_cast<const uint8_t*>(wsb + P.off_alive);
+#endif
   const void* fn = P.var->fold_fn[P.compact_ok ? 1 : 0];
   const size_t lds = (size_t)P.var->lds_fold;
   const int occ = occupancy(fn, lds, P.var->NT);

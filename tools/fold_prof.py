@@ -13,7 +13,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "build_ablate")
+OUT = os.path.join(ROOT, "build_ab")   # (travels to the GPU box; build_ablate is gpurun-ignored)
 LIB = os.path.join(OUT, os.environ.get("FOLDPROF_LIB", "lib_foldprof.so"))
 EXTRA = os.environ.get("FOLDPROF_DEFS", "").split()   # build: extra -D flags (timing-only ablations)
 FNAMES = ["fin: wait preparer", "fin: item loads + xsd wait", "fin: compute + stores", "fin: items",
@@ -29,7 +29,7 @@ def build():
            ("gnca_step.hip", "gnca_bwd.hip", "gnca_aux.hip")]
     objs = []
     for s in src:
-        o = os.path.join(OUT, os.path.basename(s) + "." + os.path.basename(LIB) + ".o")
+        o = os.path.join(ROOT, "build", os.path.basename(s) + "." + os.path.basename(LIB) + ".o")
         extra = ["-fno-slp-vectorize", "-DGNCA_PROFILE", *EXTRA] if s.endswith("gnca_step.hip") else []
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
                         *extra, f"-I{ROOT}/include", s, "-o", o], check=True, stderr=subprocess.DEVNULL)
@@ -86,7 +86,7 @@ def run():
         used = arr[:, :, 7].sum(1) > 0
         print(" per-wave arrival (cycles from the wave's start, mean over WGs): points = DMA+fire issued, prep done, "
               "finalize done, past prologue barrier, groups done, zero items done (tile 0), past tile-0 barrier, end")
-        for wv in range(8):
+        for wv in range(int(os.environ.get("FOLDPROF_WAVES", "8"))):
             print(f"  wave {wv}: " + " ".join(f"{arr[used, wv, k].mean():7.0f}" for k in range(8)))
         if steps > 1:
             for title, f in (("wave 0", ff[:, :16]), ("wave 3 (preparer)", ff[:, 16:])):
