@@ -371,6 +371,10 @@ struct BBArgs {
   float* dY;           // [B, 3C, H, W]
   float* dG;           // [B, C, H, W]
   float* dmb;          // [B, H, W] <dm, b_M> (zero-pad only) or null
+  // [B, H, W] keep bytes (fire AND pre-alive) written by the first slice, or null: then the dead
+  // cells' dY / dG / dmb are not stored at all and their readers (BC, BC2) take them as zeros
+  // from the keep plane; null (A/B builds): the dead cells' zeros are stored
+  uint8_t* keep;
   float* part;         // [gridDim.x * NW][npart]
   uint64_t seed;
   int64_t rng_step;
@@ -545,7 +549,12 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     __syncthreads();
     BPROF_MARK(7);   // loop tail
     if (a.active && !a.active[b]) {   // masked step, inactive sample: every cell is dead
-      if (first && !(a.flags & kZeroed))
+      if (first && a.keep)
+        for (int n = tid; n < ncell; n += kThreads) {
+          const int ti = n / TW, tj = n - (n / TW) * TW;
+          if (i0 + ti < H && j0 + tj < W) a.keep[(size_t)b * HW + (i0 + ti) * W + (j0 + tj)] = 0;
+        }
+      else if (first && !(a.flags & kZeroed))
         for (int n = tid; n < ncell; n += kThreads) {
           const int ti = n / TW, tj = n - (n / TW) * TW;
           if (i0 + ti >= H || j0 + tj >= W) continue;
@@ -652,7 +661,9 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     const float mu_u = a.coef[4 * b + 2], mu_ux = a.coef[4 * b + 3];
     // ---- live-cell compaction (as the forward K1): a cell with keep == 0 has d_pre = 0, so its
     //      dY / dG are zero and it adds nothing to any weight gradient; only live cells are
-    //      packed into MFMA groups, the zeros of the dead ones are stored here ----
+    //      packed into MFMA groups; the first slice stores every cell's keep byte (BC and BC2 read
+    //      a dead cell's dY / dG / dmb as zeros from it: 1 byte instead of 4 (3C + C + 1) bytes of
+    //      zeros per dead cell) ----
     int* lst = reinterpret_cast<int*>(smem + L.lst);
     int* wcnt = lst + r4(TH * TW);
     int nlive = 0;
@@ -670,9 +681,10 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
         off += w_ < wave ? wcnt[w_] : 0;
         tot += wcnt[w_];
       }
+      if (inb && first && a.keep) a.keep[(size_t)b * HW + (i0 + ti) * W + (j0 + tj)] = live ? 1 : 0;
       if (live) {
         lst[off + pre] = n;
-      } else if (inb && first && !(a.flags & kZeroed)) {
+      } else if (inb && first && !a.keep && !(a.flags & kZeroed)) {
         const int ce = (i0 + ti) * W + (j0 + tj);
         for (int pl = 0; pl < 3 * C; ++pl) dYb[pl * HWi + ce] = 0.f;
         if (msg)
@@ -1025,6 +1037,7 @@ struct BCArgs {
   const float* perc;
   const float* offw;
   const uint8_t* active;
+  const uint8_t* keep;   // [B, H, W] BB's keep bytes (a dead cell's dY / dG are zeros, not stored), or null
   float* gx;
   int B, C, H, W, k, TH, TW, tiles_x, tps, RY, RX;
   int cpw, ncg;   // channels per workgroup, channel groups (small problems: more workgroups)
@@ -1076,17 +1089,27 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   // and bit i of gsel set when the slot reads dG. Both are hoisted out of the channel loop, so
   // a load costs one select of two wave-uniform bases plus one 64-bit add.
   const int CHW = C * (int)HW;
+  // With BB's keep plane a dead source cell's slot is a zero too (its dY / dG were not stored):
+  // slot i is loaded only when bit i of sld is set (the keep bytes of the slots' cells: 16 byte
+  // loads once per workgroup, all in flight together).
   int soff[kBCStage];
-  uint32_t gsel = 0;
+  uint32_t gsel = 0, sld = 0;
+  uint8_t kv[kBCStage];
+  const uint8_t* kb = a.keep ? a.keep + (size_t)b * HW : nullptr;
 #pragma unroll
   for (int i = 0; i < kBCStage; ++i) {
     const int e = tid + kThreads * i;
     soff[i] = -1;
+    kv[i] = 1;
     if (e >= SE) continue;
+    int cell = -1;
     if (e < 3 * PA) {
       const int f = e / PA, r = e - f * PA;
       const int ii = i0 - 1 + r / PW, jj = j0 - 1 + r % PW;
-      if (ii >= 0 && ii < H && jj >= 0 && jj < W) soff[i] = f * CHW + ii * W + jj;
+      if (ii >= 0 && ii < H && jj >= 0 && jj < W) {
+        soff[i] = f * CHW + ii * W + jj;
+        cell = ii * W + jj;
+      }
     } else {
       const int r = e - 3 * PA;
       int ii = i0 - RY + r / GW, jj = j0 - RX + r % GW;
@@ -1094,9 +1117,15 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
       if (zp) ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
       else { ii = wrapi(ii, H); jj = wrapi(jj, W); }
       gsel |= 1u << i;
-      if (ok) soff[i] = ii * W + jj;
+      if (ok) {
+        soff[i] = ii * W + jj;
+        cell = ii * W + jj;
+      }
     }
+    if (kb && cell >= 0) kv[i] = kb[cell];
   }
+#pragma unroll
+  for (int i = 0; i < kBCStage; ++i) sld |= (soff[i] >= 0 && kv[i] != 0) ? 1u << i : 0u;
   float stg[kBCStage];
   auto load = [&](int c) {
     const float* pY = a.dY + ((size_t)b * 3 * C + c) * HW;
@@ -1104,7 +1133,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
 #pragma unroll
     for (int i = 0; i < kBCStage; ++i) {
       const float* p = ((gsel >> i) & 1u) ? pG : pY;
-      stg[i] = soff[i] >= 0 ? p[soff[i]] : 0.f;
+      stg[i] = ((sld >> i) & 1u) ? p[soff[i]] : 0.f;
     }
   };
   auto store = [&](float* dst) {
@@ -1204,6 +1233,7 @@ struct BC2Args {
   const float* x;
   const float* dG;
   const float* dmb;
+  const uint8_t* keep;   // BB's keep bytes (a dead cell's dG / dmb are zeros, not stored), or null
   double* dots;   // [B][k][nrb]
   int B, C, H, W, k, nrb, rows_per;
   float gthr;
@@ -1235,6 +1265,8 @@ __global__ __launch_bounds__(kThreads) void gnca_b_dots(const BC2Args a) {
       if (!(mx > a.gthr)) continue;
     }
     const size_t q = (size_t)i * W + j, t = (size_t)it * W + j;
+    // a dead target adds exactly +0 (s = 0 + sum x * 0 for finite x): skipped
+    if (a.keep && !a.keep[(size_t)b * HW + t]) continue;
     float s = a.dmb[(size_t)b * HW + t];
     for (int c = 0; c < C; ++c) s = fmaf(xb[c * HW + q], gb[c * HW + t], s);
     acc += (double)s;
@@ -1490,7 +1522,7 @@ struct BwdPlan {
   int nrb, rows_per;       // BC2
   size_t ldsD;
   int npart, o_w1, o_b1, o_w2, o_wm, o_bm, nq;
-  size_t off_fwd, off_U, off_dY, off_dG, off_dmb, off_pa, off_coef, off_pb, off_dots, off_pq, off_corr, bytes;
+  size_t off_fwd, off_U, off_dY, off_dG, off_dmb, off_keep, off_pa, off_coef, off_pb, off_dots, off_pq, off_corr, bytes;
 };
 
 static int bwd_device_cus() {
@@ -1671,6 +1703,7 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   P->off_dY = carve(3 * n * 4);
   P->off_dG = carve(P->msg ? n * 4 : 0);
   P->off_dmb = carve(P->msg && P->zp ? hw * 4 : 0);
+  P->off_keep = carve(hw);
   P->off_pa = carve((size_t)d->B * P->nbands * (2 + 2 * C) * 8);
   P->off_coef = carve((size_t)d->B * 4 * 4);
   P->off_pb = carve((size_t)P->gridB * NW * P->npart * 4);
@@ -1771,6 +1804,12 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
   float* dY = reinterpret_cast<float*>(wsb + P.off_dY);
   float* dG = reinterpret_cast<float*>(wsb + P.off_dG);
   float* dmb = (P.msg && P.zp) ? reinterpret_cast<float*>(wsb + P.off_dmb) : nullptr;
+  // BB's keep bytes (gnca_b_mlp; the split BB of A/B builds stores the dead cells' zeros instead)
+#ifndef GNCA_BB_NO_KEEP   // A/B builds: the dead cells' zeros stored by BB (round 4's scheme)
+  uint8_t* keep = P.bbfn == P.bb->fn ? reinterpret_cast<uint8_t*>(wsb + P.off_keep) : nullptr;
+#else
+  uint8_t* keep = nullptr;
+#endif
   double* pa = reinterpret_cast<double*>(wsb + P.off_pa);
   float* coef = reinterpret_cast<float*>(wsb + P.off_coef);
   float* pb = reinterpret_cast<float*>(wsb + P.off_pb);
@@ -1795,7 +1834,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     memset(&a, 0, sizeof(a));
     a.x = x; a.U = U; a.dx = dx; a.coef = coef; a.fire = fire;
     a.perc = w->perception; a.w1 = w->w1; a.b1 = w->b1; a.w2 = w->w2; a.wm = w->wm; a.bm = w->bm;
-    a.offw = offw; a.active = active; a.dY = dY; a.dG = dG; a.dmb = dmb; a.part = pb;
+    a.offw = offw; a.active = active; a.dY = dY; a.dG = dG; a.dmb = dmb; a.keep = keep; a.part = pb;
     a.seed = d.rng_seed; a.rng_step = d.rng_step; a.sample_base = d.sample_base;
     a.B = B; a.C = C; a.H = H; a.W = W; a.hidden = Hd; a.k = P.msg ? P.F.k : 0;
     a.RY = P.RY; a.RX = P.RX; a.TH = P.TH; a.TW = P.TW; a.tiles_x = P.tiles_x; a.tps = P.tps;
@@ -1835,7 +1874,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
   {
     BCArgs a;
     memset(&a, 0, sizeof(a));
-    a.dY = dY; a.dG = dG; a.x = x; a.perc = w->perception; a.offw = offw; a.gx = gx;
+    a.dY = dY; a.dG = dG; a.x = x; a.perc = w->perception; a.offw = offw; a.gx = gx; a.keep = keep;
     a.active = active;
     a.B = B; a.C = C; a.H = H; a.W = W; a.k = P.msg ? P.F.k : 0;
     a.TH = P.TH3; a.TW = P.TW3; a.tiles_x = P.tiles_x3; a.tps = P.tps3;
@@ -1888,7 +1927,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
   {
     BC2Args a;
     memset(&a, 0, sizeof(a));
-    a.x = x; a.dG = dG; a.dmb = dmb; a.dots = dots;
+    a.x = x; a.dG = dG; a.dmb = dmb; a.keep = keep; a.dots = dots;
     a.B = B; a.C = C; a.H = H; a.W = W; a.k = P.F.k; a.nrb = P.nrb; a.rows_per = P.rows_per;
     a.gthr = d.graph_alpha_thr; a.a2a = (d.flags & GNCA_ALIVE_TO_ALIVE) ? 1 : 0;
     for (int o = 0; o < 2 * P.F.k; ++o) a.offs[o] = d.offsets[o];

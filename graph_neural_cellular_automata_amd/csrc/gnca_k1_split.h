@@ -1373,13 +1373,21 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
       // (acc2: declared above)
       f32x16 acc1[2];
       // GEMM1 product q (0..17) of one row block: k-chunk q / 6, (A part, B part) by q % 6
-      auto g1p = [&](f32x16& ac, const u32x4 (&A)[3][3], int q) {
+      // (LEANV 4, A/B builds: each A fragment read from LDS right before its MFMA instead of a row
+      //  block's nine held in registers)
+      auto g1p = [&](f32x16& ac, const u32x4 (&A)[3][3], int q, int rbn) {
         const int kc = q / 6, pp = q % 6;
         const int ap = (pp == 2 || pp == 5) ? 1 : (pp == 4 ? 2 : 0);
         const int bp = (pp == 1 || pp == 5) ? 1 : (pp == 3 ? 2 : 0);
-        ac = mfma_bx(A[kc][ap], yf[kc][bp], ac);
+        u32x4 Af;
+        if constexpr (LEANV == 4)
+          Af = *reinterpret_cast<const u32x4*>(smem_b + L.w1 + (rbn * 3 + kc) * 1024 + lane * 16 + ap * 12288);
+        else
+          Af = A[kc][ap];
+        ac = mfma_bx(Af, yf[kc][bp], ac);
       };
       auto ldA = [&](int rb, u32x4 (&A)[3][3], u32x4& bz) {
+        if constexpr (LEANV == 4) return;
         bz = *reinterpret_cast<const u32x4*>(smem_b + L.bias + rb * 512 + r32 * 16);
 #pragma unroll
         for (int kc = 0; kc < 3; ++kc)
@@ -1404,8 +1412,8 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
-          g1p(acc1[0], A, 2 * k);
-          g1p(acc1[0], A, 2 * k + 1);
+          g1p(acc1[0], A, 2 * k, 0);
+          g1p(acc1[0], A, 2 * k + 1, 0);
           if constexpr (GRAPH) {
             if (k < 4) {
 #pragma unroll
@@ -1441,8 +1449,8 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             if (more) {
-              g1p(nx, A, 8 * ss + 2 * k);
-              g1p(nx, A, 8 * ss + 2 * k + 1);
+              g1p(nx, A, 8 * ss + 2 * k, rb + 1);
+              g1p(nx, A, 8 * ss + 2 * k + 1, rb + 1);
             }
             uint32_t p0, p1, p2;
             split3_pair(hv[2 * k], hv[2 * k + 1], p0, p1, p2);
@@ -1453,8 +1461,8 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
           }
           // step: this k-chunk's GEMM2 products (+ the next row block's last two, second chunk)
           if (more && ss == 1) {
-            g1p(nx, A, 16);
-            g1p(nx, A, 17);
+            g1p(nx, A, 16, rb + 1);
+            g1p(nx, A, 17, rb + 1);
           }
           acc2 = mfma_bx(T0, h0, acc2);
           acc2 = mfma_bx(T1, h0, acc2);
