@@ -847,7 +847,10 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
             for (int ft = 0; ft < FT; ++ft)
               ay[ft] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[ft][r], dh[m][r], ay[ft], 0, 0, 0);
         }
-        if (valid) {
+#ifndef GNCA_BB_ABL_STORE
+#define GNCA_BB_ABL_STORE 0   // timing-only builds: 1 = no dY / dG stores (wrong results)
+#endif
+        if (valid && !GNCA_BB_ABL_STORE) {
           float* q = dYb + celli;
           if (first && cfull && 16 * FT == 3 * CP) {
 #pragma unroll
@@ -893,7 +896,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
             for (int s = 0; s < 4; ++s)
               ag = __builtin_amdgcn_mfma_f32_16x16x4f32(wms[(16 * mo + 4 * g + s) * SWM + 16 * mi + c16],
                                                         dm[mo][s], ag, 0, 0, 0);
-          if (valid) {
+          if (valid && !GNCA_BB_ABL_STORE) {
             float* q = dGb + (16 * mi + 4 * g) * HWi + celli;
             if (cfull && (CP & 15) == 0) {
 #pragma unroll
@@ -1052,6 +1055,9 @@ __host__ __device__ inline int bc_stage(int TH, int TW, int RY, int RX, bool msg
   return 3 * (TH + 2) * (TW + 2) + (msg ? (TH + 2 * RY) * (TW + 2 * RX) : 0);
 }
 
+#ifndef GNCA_BC_ABL
+#define GNCA_BC_ABL 0   // timing-only builds: 1 = no staging loads, 2 = no stencil arithmetic (wrong results)
+#endif
 // One workgroup per (sample, tile); channels are pipelined through a double-buffered LDS
 // stage (the next channel's dY planes and dG halo are loaded into registers while this channel
 // is computed), one barrier per channel.
@@ -1133,7 +1139,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
 #pragma unroll
     for (int i = 0; i < kBCStage; ++i) {
       const float* p = ((gsel >> i) & 1u) ? pG : pY;
-      stg[i] = ((sld >> i) & 1u) ? p[soff[i]] : 0.f;
+      stg[i] = ((sld >> i) & 1u) && !(GNCA_BC_ABL & 1) ? p[soff[i]] : 0.f;
     }
   };
   auto store = [&](float* dst) {
@@ -1184,7 +1190,23 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
     }
   }
   store(buf0);
-  __syncthreads();
+  // the reference's frozen identity / Sobel bank (the module's perception, always, in practice)?
+  // Then the adjoint reads only the 13 taps with nonzero weights, with the weights as constants:
+  // the same nonzero products in the same order as the generic loop (a zero-weight tap adds +0 to
+  // a sum that is never -0), so bitwise the same gx
+  int pok = 1;
+  for (int e = tid; e < C * 27; e += kThreads) {
+    const int f = (e % 27) / 9, tap = e % 9, tr = tap / 3, tc = tap % 3;
+    const float ref = f == 0 ? (tap == 4 ? 1.f : 0.f)
+                    : f == 1 ? (float)((tc == 0 ? 1 : (tc == 2 ? -1 : 0)) * (tr == 1 ? 2 : 1))
+                             : (float)((tr == 0 ? 1 : (tr == 2 ? -1 : 0)) * (tc == 1 ? 2 : 1));
+    if (pws[e] != ref) pok = 0;
+  }
+#ifdef GNCA_BC_GENERIC   // A/B builds: the generic 27-tap loop always
+  const bool sobel = __syncthreads_and(pok) != 0 && false;
+#else
+  const bool sobel = __syncthreads_and(pok) != 0;
+#endif
   for (int c = c_lo; c < c_hi; ++c) {
     float* cur = ((c - c_lo) & 1) ? buf1 : buf0;
     float* nxt = ((c - c_lo) & 1) ? buf0 : buf1;
@@ -1201,14 +1223,34 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
       const int ti = gtij[u] >> 16, tj = gtij[u] & 0xffff;
       // y(p) += w[u][v] x(p + (u-1, v-1))  =>  gx(q) += w[u][v] dY(q - (u-1, v-1))
       float acc = 0.f;
+      if (GNCA_BC_ABL & 2) {
+      } else if (sobel) {
+        // tap (u, v) of plane f reads cur[f PA + (ti + 2 - u) PW + (tj + 2 - v)]
+        const float* c0 = cur + (ti + 2) * PW + (tj + 2);
+        auto Y = [&](int f, int u, int v) { return c0[f * PA - u * PW - v]; };
+        acc = fmaf(1.f, Y(0, 1, 1), acc);
+        acc = fmaf(1.f, Y(1, 0, 0), acc);
+        acc = fmaf(-1.f, Y(1, 0, 2), acc);
+        acc = fmaf(2.f, Y(1, 1, 0), acc);
+        acc = fmaf(-2.f, Y(1, 1, 2), acc);
+        acc = fmaf(1.f, Y(1, 2, 0), acc);
+        acc = fmaf(-1.f, Y(1, 2, 2), acc);
+        acc = fmaf(1.f, Y(2, 0, 0), acc);
+        acc = fmaf(2.f, Y(2, 0, 1), acc);
+        acc = fmaf(1.f, Y(2, 0, 2), acc);
+        acc = fmaf(-1.f, Y(2, 2, 0), acc);
+        acc = fmaf(-2.f, Y(2, 2, 1), acc);
+        acc = fmaf(-1.f, Y(2, 2, 2), acc);
+      } else {
 #pragma unroll
-      for (int f = 0; f < 3; ++f)
+        for (int f = 0; f < 3; ++f)
 #pragma unroll
-        for (int u = 0; u < 3; ++u)
+          for (int u = 0; u < 3; ++u)
 #pragma unroll
-          for (int v = 0; v < 3; ++v)
-            acc = fmaf(pw[f * 9 + u * 3 + v], cur[f * PA + (ti + 2 - u) * PW + (tj + 2 - v)], acc);
-      if (msg) {
+            for (int v = 0; v < 3; ++v)
+              acc = fmaf(pw[f * 9 + u * 3 + v], cur[f * PA + (ti + 2 - u) * PW + (tj + 2 - v)], acc);
+      }
+      if (msg && !(GNCA_BC_ABL & 2)) {
         // msg(p) = sum_o w_o A(p-o) M(p-o)  =>  gM(q) = A(q) sum_o w_o dm(q+o)  (roll / row shift)
         const float* g0 = cur + 3 * PA + (ti + RY) * GW + (tj + RX);
         float sg = 0.f;
