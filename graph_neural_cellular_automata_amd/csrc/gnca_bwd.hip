@@ -50,6 +50,7 @@ __device__ float g_bzero[4];   // LDS-DMA source for off-image cells (zero-initi
 constexpr uint32_t kMsg = 1u << 16;      // message path active (k > 0 and message_gain != 0)
 constexpr uint32_t kFirst = 1u << 17;    // first hidden slice: also the message backward
 constexpr uint32_t kGN = 1u << 18;       // GroupNorm on
+constexpr uint32_t kDma4 = 1u << 20;     // BB: 16-byte LDS-DMA staging (W, TW and the x halo multiples of 4)
 constexpr uint32_t kZeroed = 1u << 19;   // dY / dG / dmb were zero-filled before BB: no dead-cell zero stores
 
 // Measurement-only phase timers of BB (tools/bprof.py builds with -DGNCA_PROFILE): wave 0 of each
@@ -568,7 +569,35 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     }
     // ---- staging by LDS-DMA (as the forward K1): every channel plane of the (RH x RW) region
     //      and the alpha plane with one more ring, all loads in flight at once, no VGPR round
-    //      trip; torus-wrapped, or a zero source outside the image in pad mode ----
+    //      trip; torus-wrapped, or a zero source outside the image in pad mode.  16-byte pieces
+    //      (kDma4: the region's quads never straddle a row end or the image edge) take a quarter
+    //      of the instructions of 4-byte ones, whose issue was a fifth of BB at B=1024 ----
+    if (a.flags & kDma4) {
+      const int QW = RW >> 2, NQ = RH * QW, NI4 = (NQ + 63) >> 6;
+      for (int ii_ = wave; ii_ < NI4; ii_ += NW) {
+        const int q = 64 * ii_ + lane;
+        if (q < NQ) {
+          const int vr = q / QW, vc = 4 * (q - (q / QW) * QW);
+          int ii = i0 - RY + vr, jj = j0 - RX + vc, off = 0;
+          bool ok = true;
+          if (zp) {
+            ok = ii >= 0 && ii < H && jj >= 0 && jj < W;
+            off = ok ? ii * W + jj : 0;
+          } else {
+            while (ii < 0) ii += H; while (ii >= H) ii -= H;
+            while (jj < 0) jj += W; while (jj >= W) jj -= W;
+            off = ii * W + jj;
+          }
+          float* dst = xs + 256 * ii_;
+          for (int c = 0; c < CP; ++c) {
+            const float* src = xb + (size_t)min(c, C - 1) * HW + off;
+            if ((zp && !ok) || c >= C) src = g_bzero;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(dst + c * PSTR), 16, 0, 0);
+          }
+        }
+      }
+    } else
     for (int ii_ = wave; ii_ < L.NI; ii_ += NW) {
       const int e = 64 * ii_ + lane;
       int off = 0;
@@ -1555,6 +1584,7 @@ struct BwdPlan {
   int CP, HB, nslices;
   bool graph, msg, zp, gn;
   int RY, RX;
+  int RXB;   // BB's x halo (RX padded to a multiple of 4 when W is one: 16-byte staging)
   int TH, TW, tiles_x, tps, total_tiles, gridB;
   size_t ldsB;
   int band, nbands;        // BA
@@ -1597,6 +1627,8 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
     }
   P->RY = ry;
   P->RX = rx;
+  // BB's staged x halo: padded to a multiple of 4 columns when the rows are (16-byte LDS-DMA pieces)
+  const int rxb = (W % 4 == 0) ? ((rx + 3) & ~3) : rx;
   // hidden slice (variant) and BB tile: fewest slices first (each slice recomputes the
   // perception, gather and message), then fewest padded hidden units, then the cheapest tile
   // (padded cells + staged halo) within 160 KB of LDS
@@ -1613,9 +1645,9 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
     const int padh = ns * v.HB - Hd;
     for (int th : ths)
       for (int tw : tws) {
-        if ((th * tw) % 64 || tw + 2 * rx + 2 > 64) continue;   // staging rows fit one wave
+        if ((th * tw) % 64 || tw + 2 * rxb + 2 > 64) continue;   // staging rows fit one wave
         if (eth && (th != eth || tw != etw)) continue;
-        const BBLayout L = bb_layout(P->CP, v.HB, th, tw, ry, rx, P->F.k);
+        const BBLayout L = bb_layout(P->CP, v.HB, th, tw, ry, rxb, P->F.k);
         const size_t bytes = (size_t)L.total * 4;
         if (bytes > 160 * 1024) continue;
         const long tx = (W + tw - 1) / tw, ty = (H + th - 1) / th;
@@ -1634,6 +1666,7 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   }
   if (!P->bb) return false;
   P->bbfn = P->bbfn2 = P->bb->fn;
+  P->RXB = rxb;
   // C = 16, hidden = 128: the split-arithmetic BB (gnca_bb_split.h), two 64-unit hidden slices (the
   // per-wave weight-gradient accumulators of the whole hidden layer do not fit the register file),
   // its own tile (the cheapest by the same makespan model within its LDS: weight images 28 KB + 4 x
@@ -1672,6 +1705,7 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
                         : reinterpret_cast<const void*>(&gnca_b_split<false, false>);
       P->HB = kBSHB;
       P->nslices = 128 / kBSHB;
+      P->RXB = rx;   // its own staging (4-byte pieces, the unpadded halo)
     }
   }
 #endif
@@ -1879,7 +1913,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     a.offw = offw; a.active = active; a.dY = dY; a.dG = dG; a.dmb = dmb; a.keep = keep; a.part = pb;
     a.seed = d.rng_seed; a.rng_step = d.rng_step; a.sample_base = d.sample_base;
     a.B = B; a.C = C; a.H = H; a.W = W; a.hidden = Hd; a.k = P.msg ? P.F.k : 0;
-    a.RY = P.RY; a.RX = P.RX; a.TH = P.TH; a.TW = P.TW; a.tiles_x = P.tiles_x; a.tps = P.tps;
+    a.RY = P.RY; a.RX = P.RXB; a.TH = P.TH; a.TW = P.TW; a.tiles_x = P.tiles_x; a.tps = P.tps;
     a.total_tiles = P.total_tiles; a.fire_mode = d.fire_mode;
     a.npart = P.npart; a.o_w1 = P.o_w1; a.o_b1 = P.o_b1; a.o_w2 = P.o_w2; a.o_wm = P.o_wm; a.o_bm = P.o_bm;
     a.fire_rate = d.fire_rate; a.alpha_thr = d.alpha_thr; a.graph_alpha_thr = d.graph_alpha_thr;
@@ -1899,8 +1933,11 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
       return GNCA_ERR_HIP;
     a.flags |= kZeroed;
 #endif
-    const int RW = P.TW + 2 * P.RX;
+    const int RW = P.TW + 2 * P.RXB;
     for (int o = 0; o < a.k; ++o) a.odl[o] = d.offsets[2 * o] * RW + (P.zp ? 0 : d.offsets[2 * o + 1]);
+#ifndef GNCA_BB_NO_DMA4   // A/B builds: 4-byte staging pieces (round 4's BB)
+    if (W % 4 == 0 && P.RXB % 4 == 0 && P.TW % 4 == 0 && P.bbfn == P.bb->fn) a.flags |= kDma4;
+#endif
     (void)hipFuncSetAttribute(P.bbfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.ldsB);
     (void)hipFuncSetAttribute(P.bbfn2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.ldsB);
     for (int s = 0; s < P.nslices; ++s) {

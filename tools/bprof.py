@@ -12,7 +12,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "build_ablate")
+OUT = os.path.join(ROOT, "build_ab")   # (travels to the GPU box; build_ablate is gpurun-ignored)
 LIB = os.path.join(OUT, "libgnca_prof.so")
 NAMES = ["weights", "dma_issue+fire", "dma_wait", "planes+compaction", "groups", "epilogue", "-", "loop_tail"]
 
@@ -22,7 +22,7 @@ def build():
     csrc = os.path.join(ROOT, "graph_neural_cellular_automata_amd", "csrc")
     srcs = [os.path.join(csrc, f) for f in ("gnca_step.hip", "gnca_bwd.hip", "gnca_aux.hip")]
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-                           "-shared", "-DGNCA_PROFILE", f"-I{ROOT}/include", f"-I{csrc}", *srcs, "-o", LIB])
+                           "-shared", "-DGNCA_PROFILE", "-fno-slp-vectorize", f"-I{ROOT}/include", f"-I{csrc}", *srcs, "-o", LIB])
 
 
 def run(sizes):
