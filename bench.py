@@ -65,7 +65,7 @@ WORKLOADS = {
 # (tools/pmc.sh + tools/pmc_traffic.py); counters cannot be read from inside this process
 # the passes of the shipped build (round 4's final tag r04h; a round's tags are not in time order, so
 # the name is explicit), else the highest-named file
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04h_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05z_pmc_traffic.json")
 if not os.path.exists(PMC_TRAFFIC):
     PMC_TRAFFIC = max(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc_traffic.json")) or
                       [os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")])
