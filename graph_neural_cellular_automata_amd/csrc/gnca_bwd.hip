@@ -387,7 +387,9 @@ struct BBArgs {
   int odl[GNCA_MAX_OFFSETS];
 };
 
-template <int CP, int HB>
+// FULL: C == CP (no padded channels), so every per-lane channel test is a compile-time constant: at
+// runtime C those tests were 64-bit lane masks held across the group loop (SGPR spills)
+template <int CP, int HB, bool FULL = false>
 __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CPQ = CP / 4, KS = 3 * CPQ, MT = HB / 16, MO = (CP + 15) / 16, FT = (3 * CP + 15) / 16;
@@ -411,7 +413,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   BPROF_DECL
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int C = a.C, H = a.H, W = a.W, Hd = a.hidden, h0 = a.h0, k = a.k;
+  const int C = FULL ? CP : a.C, H = a.H, W = a.W, Hd = a.hidden, h0 = a.h0, k = a.k;
   const bool zp = (a.flags & GNCA_ZERO_PAD_SHIFT) != 0;
   const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
@@ -1566,8 +1568,10 @@ __global__ __launch_bounds__(kThreads) void gnca_b_reduce(const RedArgs a) {
 struct BBVariant {
   int CP, HB;
   const void* fn;
+  const void* fnf;   // the C == CP instance (16 and 32 channels), or null
 };
-#define GNCA_BV(cp, hb) {cp, hb, reinterpret_cast<const void*>(&gnca_b_mlp<cp, hb>)}
+#define GNCA_BV(cp, hb) {cp, hb, reinterpret_cast<const void*>(&gnca_b_mlp<cp, hb>), \
+                         (cp == 16 || cp == 32) ? reinterpret_cast<const void*>(&gnca_b_mlp<cp, hb, true>) : nullptr}
 static const BBVariant kBB[] = {
     GNCA_BV(16, 128), GNCA_BV(4, 32),  GNCA_BV(8, 32),  GNCA_BV(16, 32), GNCA_BV(4, 64),
     GNCA_BV(8, 64),   GNCA_BV(12, 64), GNCA_BV(16, 64), GNCA_BV(20, 64), GNCA_BV(24, 64),
@@ -1581,6 +1585,7 @@ struct BwdPlan {
   const BBVariant* bb;
   const void* bbfn;    // the BB kernel: gnca_b_split<MSG, true> (C = 16, hidden = 128) or bb->fn
   const void* bbfn2;   // the kernel of slices after the first (gnca_b_split<MSG, false>, or bb->fn)
+  bool bbf32;          // BB is gnca_b_mlp (keep bytes, 16-byte staging), not the split A/B kernel
   int CP, HB, nslices;
   bool graph, msg, zp, gn;
   int RY, RX;
@@ -1665,7 +1670,12 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
       }
   }
   if (!P->bb) return false;
+#ifdef GNCA_BB_NO_FULL   // A/B builds: the runtime-C instance always
   P->bbfn = P->bbfn2 = P->bb->fn;
+#else
+  P->bbfn = P->bbfn2 = (C == P->CP && P->bb->fnf) ? P->bb->fnf : P->bb->fn;
+#endif
+  P->bbf32 = true;
   P->RXB = rxb;
   // C = 16, hidden = 128: the split-arithmetic BB (gnca_bb_split.h), two 64-unit hidden slices (the
   // per-wave weight-gradient accumulators of the whole hidden layer do not fit the register file),
@@ -1706,10 +1716,11 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
       P->HB = kBSHB;
       P->nslices = 128 / kBSHB;
       P->RXB = rx;   // its own staging (4-byte pieces, the unpadded halo)
+      P->bbf32 = false;
     }
   }
 #endif
-  if (P->bbfn == P->bb->fn) {
+  if (P->bbf32) {
   P->HB = P->bb->HB;
   P->nslices = (Hd + P->HB - 1) / P->HB;
   }
@@ -1882,7 +1893,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
   float* dmb = (P.msg && P.zp) ? reinterpret_cast<float*>(wsb + P.off_dmb) : nullptr;
   // BB's keep bytes (gnca_b_mlp; the split BB of A/B builds stores the dead cells' zeros instead)
 #ifndef GNCA_BB_NO_KEEP   // A/B builds: the dead cells' zeros stored by BB (round 4's scheme)
-  uint8_t* keep = P.bbfn == P.bb->fn ? reinterpret_cast<uint8_t*>(wsb + P.off_keep) : nullptr;
+  uint8_t* keep = P.bbf32 ? reinterpret_cast<uint8_t*>(wsb + P.off_keep) : nullptr;
 #else
   uint8_t* keep = nullptr;
 #endif
@@ -1936,7 +1947,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     const int RW = P.TW + 2 * P.RXB;
     for (int o = 0; o < a.k; ++o) a.odl[o] = d.offsets[2 * o] * RW + (P.zp ? 0 : d.offsets[2 * o + 1]);
 #ifndef GNCA_BB_NO_DMA4   // A/B builds: 4-byte staging pieces (round 4's BB)
-    if (W % 4 == 0 && P.RXB % 4 == 0 && P.TW % 4 == 0 && P.bbfn == P.bb->fn) a.flags |= kDma4;
+    if (W % 4 == 0 && P.RXB % 4 == 0 && P.TW % 4 == 0 && P.bbf32) a.flags |= kDma4;
 #endif
     (void)hipFuncSetAttribute(P.bbfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.ldsB);
     (void)hipFuncSetAttribute(P.bbfn2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.ldsB);
