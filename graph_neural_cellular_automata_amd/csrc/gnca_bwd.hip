@@ -389,12 +389,14 @@ struct BBArgs {
 
 // FULL: C == CP (no padded channels), so every per-lane channel test is a compile-time constant: at
 // runtime C those tests were 64-bit lane masks held across the group loop (SGPR spills)
-template <int CP, int HB, bool FULL = false>
+// TH_ .. K_ (all > 0, K_ >= 0): the tile geometry and offset count at compile time (the planned
+// shapes of the C = 16 graph and classic steps, kBBS below): every LDS offset and loop bound a constant
+template <int CP, int HB, bool FULL = false, int TH_ = 0, int TW_ = 0, int RY_ = 0, int RX_ = 0, int K_ = -1>
 __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CPQ = CP / 4, KS = 3 * CPQ, MT = HB / 16, MO = (CP + 15) / 16, FT = (3 * CP + 15) / 16;
-  const int TH = a.TH, TW = a.TW, RY = a.RY, RX = a.RX;
-  const BBLayout L = bb_layout(CP, HB, TH, TW, RY, RX, a.k);
+  const int TH = TH_ ? TH_ : a.TH, TW = TW_ ? TW_ : a.TW, RY = RY_ ? RY_ : a.RY, RX = RX_ ? RX_ : a.RX;
+  const BBLayout L = bb_layout(CP, HB, TH, TW, RY, RX, K_ >= 0 ? K_ : a.k);
   const int RH = L.RH, RW = L.RW, PSTR = L.PSTR, ALW = L.ALW;
   const int KSP = L.KSP, S1T = L.S1T, S2T = L.S2T, SWM = L.SWM, ST1 = L.ST1, ST2 = L.ST2, ST3 = L.ST3;
   float* xs = smem + L.xs;
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   BPROF_DECL
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int C = FULL ? CP : a.C, H = a.H, W = a.W, Hd = a.hidden, h0 = a.h0, k = a.k;
+  const int C = FULL ? CP : a.C, H = a.H, W = a.W, Hd = a.hidden, h0 = a.h0, k = K_ >= 0 ? K_ : a.k;
   const bool zp = (a.flags & GNCA_ZERO_PAD_SHIFT) != 0;
   const bool a2a = (a.flags & GNCA_ALIVE_TO_ALIVE) != 0;
   const bool hidden_only = (a.flags & GNCA_HIDDEN_ONLY) != 0;
@@ -1579,6 +1581,18 @@ static const BBVariant kBB[] = {
     GNCA_BV(28, 32),  GNCA_BV(32, 32),
 };
 #undef GNCA_BV
+// compile-time-geometry instances of the planned shapes (16 channels, hidden 128, x halo padded to 4):
+// 72^2 canvases take 8x24 tiles, the trainer's 40^2 8x16; graph r <= 4 (the y halo padded to 4) with
+// 8 offsets, or classic (y halo 1, no offsets)
+struct BBSpec {
+  int TH, TW, RY, RX, K;
+  const void* fn;
+};
+#define GNCA_BS(th, tw, ry, rx, k) {th, tw, ry, rx, k, reinterpret_cast<const void*>(&gnca_b_mlp<16, 128, true, th, tw, ry, rx, k>)}
+static const BBSpec kBBS[] = {
+    GNCA_BS(8, 24, 4, 4, 8), GNCA_BS(8, 16, 4, 4, 8), GNCA_BS(8, 24, 1, 4, 0), GNCA_BS(8, 16, 1, 4, 0),
+};
+#undef GNCA_BS
 
 struct BwdPlan {
   FwdLayout F;
@@ -1634,6 +1648,10 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   P->RX = rx;
   // BB's staged x halo: padded to a multiple of 4 columns when the rows are (16-byte LDS-DMA pieces)
   const int rxb = (W % 4 == 0) ? ((rx + 3) & ~3) : rx;
+  // a graph step of the compile-time BB shapes (kBBS: 16 channels, hidden 128, 8 offsets within
+  // radius 4) stages a 4-row y halo whatever its drawn offsets reach (usually 4 anyway)
+  if (P->msg && C == 16 && Hd == 128 && P->F.k == 8 && ry <= 4 && W % 4 == 0) ry = 4;
+  P->RY = ry;
   // hidden slice (variant) and BB tile: fewest slices first (each slice recomputes the
   // perception, gather and message), then fewest padded hidden units, then the cheapest tile
   // (padded cells + staged halo) within 160 KB of LDS
@@ -1674,6 +1692,13 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   P->bbfn = P->bbfn2 = P->bb->fn;
 #else
   P->bbfn = P->bbfn2 = (C == P->CP && P->bb->fnf) ? P->bb->fnf : P->bb->fn;
+#ifndef GNCA_BB_NO_SPEC   // A/B builds: no compile-time-geometry instance
+  if (C == 16 && P->CP == 16 && P->bb->HB == 128 && Hd == 128)
+    for (const BBSpec& sp : kBBS)
+      if (sp.TH == P->TH && sp.TW == P->TW && sp.RY == P->RY && sp.RX == rxb && sp.K == P->F.k &&
+          (P->msg ? sp.K > 0 : sp.K == 0))
+        P->bbfn = P->bbfn2 = sp.fn;
+#endif
 #endif
   P->bbf32 = true;
   P->RXB = rxb;
