@@ -1088,6 +1088,9 @@ __host__ __device__ inline int bc_stage(int TH, int TW, int RY, int RX, bool msg
   return 3 * (TH + 2) * (TW + 2) + (msg ? (TH + 2 * RY) * (TW + 2 * RX) : 0);
 }
 
+#ifndef GNCA_BC_DMA
+#define GNCA_BC_DMA 0   // 1 (A/B builds): the slots staged by 4-byte LDS-DMA (B=1024 bwd 4.19 vs 3.98-4.00 ms: slower)
+#endif
 #ifndef GNCA_BC_ABL
 #define GNCA_BC_ABL 0   // timing-only builds: 1 = no staging loads, 2 = no stencil arithmetic (wrong results)
 #endif
@@ -1180,6 +1183,23 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
     for (int i = 0; i < kBCStage; ++i)
       if (tid + kThreads * i < SE) dst[tid + kThreads * i] = stg[i];
   };
+  // GNCA_BC_DMA: the same slots staged by LDS-DMA straight into the buffer (a zero source for the
+  // slots that read zero): no VGPR round trip, the wait moves from the LDS stores to the channel's end
+  const int wave = tid >> 6;
+  auto dma = [&](int c, float* dst) {
+    const float* pY = a.dY + ((size_t)b * 3 * C + c) * HW;
+    const float* pG = a.dG + ((size_t)b * C + c) * HW;
+#pragma unroll
+    for (int i = 0; i < kBCStage; ++i) {
+      if (kThreads * i >= SE) break;
+      if (tid + kThreads * i < SE) {
+        const float* p = ((gsel >> i) & 1u) ? pG : pY;
+        const float* src = ((sld >> i) & 1u) ? p + soff[i] : g_bzero;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(dst + kThreads * i + 64 * wave), 4, 0, 0);
+      }
+    }
+  };
   // gx is read-modify-written; its next-channel values are prefetched with the staging loads
   // (th*tw <= 4*kThreads: at most 4 cells per thread). Per cell: offset in the channel plane
   // (-1 = none) and the tile-local index ti*TW + tj, hoisted out of the channel loop.
@@ -1200,7 +1220,8 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   };
   // the first channel's staging loads go out before the perception weights / sender mask, so
   // the prologue waits out one memory latency, not three
-  load(c_lo);
+  if (GNCA_BC_DMA) dma(c_lo, buf0);
+  else load(c_lo);
   load_gx(c_lo, gxc);
   lds_fill<kThreads, 2>(pws, C * 27, tid, [&](int e) { return a.perc[e]; });
   if (msg) {
@@ -1222,7 +1243,8 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
       as_[n] = a2a ? (mx > a.graph_alpha_thr ? 1.f : 0.f) : 1.f;
     }
   }
-  store(buf0);
+  if (GNCA_BC_DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else store(buf0);
   // the reference's frozen identity / Sobel bank (the module's perception, always, in practice)?
   // Then the adjoint reads only the 13 taps with nonzero weights, with the weights as constants:
   // the same nonzero products in the same order as the generic loop (a zero-weight tap adds +0 to
@@ -1244,7 +1266,8 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
     float* cur = ((c - c_lo) & 1) ? buf1 : buf0;
     float* nxt = ((c - c_lo) & 1) ? buf0 : buf1;
     if (c + 1 < c_hi) {
-      load(c + 1);
+      if (GNCA_BC_DMA) dma(c + 1, nxt);
+      else load(c + 1);
       load_gx(c + 1, gxn);
     }
     const float* pw = pws + c * 27;
@@ -1297,7 +1320,8 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) gxc[u] = gxn[u];
-    if (c + 1 < c_hi) store(nxt);
+    if (GNCA_BC_DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (c + 1 < c_hi) store(nxt);
     __syncthreads();
   }
 }
