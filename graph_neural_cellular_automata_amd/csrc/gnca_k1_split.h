@@ -96,9 +96,11 @@ __device__ __forceinline__ f32x16 mfma_bx(u32x4 a, u32x4 b, f32x16 c) {
 // fences keep the order), so reads are always in flight.  Left to itself the compiler emitted read /
 // wait / FMA chains (a wave alone on its SIMD then pays every LDS latency: 32-channel K1, ~2/3 of
 // each phase).  Same FMA order as the plain loop: bitwise the same sums.
-template <int KU, int PSTR>
+// ZP (zero-padded shift): the per-sample offset weights wo[o] (K0's softmax) weigh each offset's sender
+// byte (the uniform 1/k of the torus mode is applied once by the caller instead)
+template <int KU, int PSTR, bool ZP = false>
 __device__ __forceinline__ void ks_gather8(const int* odl, const float* xq, const uint8_t* spq, float (&gv)[8],
-                                           float& S) {
+                                           float& S, const float* wo = nullptr) {
   constexpr int D = GNCA_K1_PIPE_LDS;   // offsets whose reads are in flight ahead of the FMAs
   float xv[D + 1][8];
   uint32_t sv[D + 1];
@@ -114,7 +116,7 @@ __device__ __forceinline__ void ks_gather8(const int* odl, const float* xq, cons
   for (int o = 0; o < KU; ++o) {
     if (o + D < KU) ld(o + D);
     __builtin_amdgcn_sched_barrier(0);
-    const float s_ = (float)sv[o % (D + 1)];
+    const float s_ = ZP ? wo[o] * (float)sv[o % (D + 1)] : (float)sv[o % (D + 1)];
     S += s_;
 #pragma unroll
     for (int j = 0; j < 8; ++j) gv[j] = fmaf(s_, xv[o % (D + 1)][j], gv[j]);
@@ -365,7 +367,9 @@ __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst)
 #define GNCA_K1_LB GNCA_K1_SPLIT_NT   // A/B builds: launch bounds above the launched size (a VGPR cap)
 #endif
 
-template <int TH, int TW, int RY, int RX, int KU, int FOLD = 0>
+// ZP: the zero-padded shift (graph_augmentation.py's zero_padded_shift): per-sample offset weights
+// from K0 and no sender outside the image (the torus-wrapped staging there is multiplied by 0)
+template <int TH, int TW, int RY, int RX, int KU, int FOLD = 0, bool ZP = false>
 __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_b[];
   constexpr int C = 16, HD = 128, NT = GNCA_K1_SPLIT_NT, NW = NT / 64;
@@ -381,6 +385,7 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
   static_assert(7 * PSTR * 4 + 4 * RHW < 65536, "channel offsets fit the DS immediate");
   static_assert(TW <= 64, "one ballot per tile row (compact update field)");
   constexpr bool GRAPH = KU > 0;
+  static_assert(!ZP || (GRAPH && !FOLD), "the zero-padded shift: graph steps, no fold (K0 runs per step)");
   // The preparer is wave 3, the OLDER wave of SIMD 3 (waves w and w + 4 share SIMD w; the younger
   // one gets the leftover issue slots): it prepares the next tile first, then joins the groups.
   constexpr int PW = 3;
@@ -945,17 +950,21 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
         if (e < NQA) {
           const int vr = e / QW, vc = 4 * (e - (e / QW) * QW);
           int ii = i0 - RY + vr, jj = j0 - RX + vc;
+          // (ZP: a quad is inside the image or outside it as a whole, W % TW == 0)
+          if (ZP && (ii < 0 || ii >= H || jj < 0 || jj >= W)) v[u] = 0x80000000u;   // (marker: no sender)
           ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
           jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-          v[u] = *reinterpret_cast<const uint32_t*>(alb + ii * W + jj);
+          if (!ZP || v[u] == 0u) v[u] = *reinterpret_cast<const uint32_t*>(alb + ii * W + jj);
         }
       }
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const int e = 64 * u + lane;
         if (e < NQA) {
-          abw[e] = v[u];
-          if constexpr (GRAPH) spp[e] = a2a ? (v[u] >> 1) & 0x01010101u : 0x01010101u;   // 4 sender bytes
+          const bool out = ZP && v[u] == 0x80000000u;
+          abw[e] = out ? 0u : v[u];
+          if constexpr (GRAPH)   // 4 sender bytes
+            spp[e] = out ? 0u : (a2a ? (v[u] >> 1) & 0x01010101u : 0x01010101u);
         }
       }
     }
@@ -1198,7 +1207,7 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
         const float* xq = xs + hb + pidx;
         const uint8_t* spq = sp + pidx;
         if (GNCA_K1_PIPE_LDS && !(GNCA_ABLATE & 4096)) {
-          ks_gather8<KU, PSTR>(a.odl, xq, spq, gv, S);
+          ks_gather8<KU, PSTR, ZP>(a.odl, xq, spq, gv, S, ZP ? a.offw + (size_t)b * KU : nullptr);
         } else {
 #pragma unroll
           for (int o = 0; o < KU; ++o) {
@@ -1215,10 +1224,12 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
             }
           }
         }
-        const float wu = a.uniform_w;
+        if constexpr (!ZP) {
+          const float wu = a.uniform_w;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) gv[j] *= wu;
-        S *= wu;
+          for (int j = 0; j < 8; ++j) gv[j] *= wu;
+          S *= wu;
+        }
         split3_x8(gv, g0, g1, g2);
         // materialise here (before the perception's sobel / generic branch): otherwise the
         // gather arithmetic is sunk past the branch and its loaded floats stay live longer

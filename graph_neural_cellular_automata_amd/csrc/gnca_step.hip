@@ -1336,63 +1336,90 @@ struct K0Args {
 
 __global__ __launch_bounds__(kThreads) void gnca_k0_offset_weights(const K0Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int C = a.C, H = a.H, W = a.W, D = a.d, K = a.k;
   double* rs = reinterpret_cast<double*>(smem);         // [C][H] row sums
-  double* xbar = rs + (size_t)a.C * a.H;                 // [C]
-  double* qbar = xbar + a.C;                             // [d]
-  double* logit = qbar + a.d;                            // [k]
+  double* xbar = rs + (size_t)C * H;                     // [C]
+  double* qbar = xbar + C;                               // [d]
+  double* logit = qbar + D;                              // [k]
+  double* sco = logit + K;                               // [C][k] sum of a channel's rows an offset keeps
+  double* kkb = sco + (size_t)C * K;                     // [k][d] pooled key of each offset
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int C = a.C, H = a.H, W = a.W;
   const size_t HW = (size_t)H * W;
   const float* xb = a.x + (size_t)b * C * HW;
   const int lane = tid & 63, wave = tid >> 6;
-  // one wave per (c, row): lanes stride the row, fixed-order shuffle tree
-  for (int cr = wave; cr < C * H; cr += kThreads / 64) {
-    const int c = cr / H, r = cr - c * H;
-    double s = 0.0;
-    for (int j = lane; j < W; j += 64) s += (double)xb[c * HW + (size_t)r * W + j];
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0) rs[cr] = s;
+  // row sums: one wave per (c, row), lanes stride the row, fixed-order shuffle tree; a wave takes
+  // U rows at a time with all their loads in flight (one row at a time paid a memory round trip
+  // per row: 0.45 ms for B=16 40^2); the same sums bit for bit
+  constexpr int U = 8;
+  for (int base = wave * U; base < C * H; base += (kThreads / 64) * U) {
+    double s[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s[u] = 0.0;
+    for (int j = lane; j < W; j += 64) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int cr = base + u;
+        v[u] = cr < C * H ? xb[(size_t)(cr / H) * HW + (size_t)(cr - (cr / H) * H) * W + j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) s[u] += (double)v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      for (int off = 32; off > 0; off >>= 1) s[u] += __shfl_xor(s[u], off);
+    if (lane == 0)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (base + u < C * H) rs[base + u] = s[u];
   }
   __syncthreads();
+  // channel means; per (channel, offset) the sum of the rows the zero-padded shift keeps
   for (int c = tid; c < C; c += kThreads) {
     double s = 0.0;
     for (int r = 0; r < H; ++r) s += rs[c * H + r];
     xbar[c] = s / (double)HW;
   }
+  for (int e = tid; e < C * K; e += kThreads) {
+    const int c = e / K, o = e - (e / K) * K;
+    const int dy = a.offs[2 * o];
+    const int lo = dy > 0 ? 0 : -dy, hi = dy > 0 ? H - dy : H;  // valid source rows [lo,hi)
+    double S = 0.0;
+    for (int r = lo; r < hi; ++r) S += rs[c * H + r];
+    sco[c * K + o] = S;
+  }
   __syncthreads();
-  for (int e = tid; e < a.d; e += kThreads) {
+  for (int e = tid; e < D; e += kThreads) {
     double s = (double)a.bq[e];
     for (int c = 0; c < C; ++c) s += (double)a.wq[e * C + c] * xbar[c];
     qbar[e] = s;
   }
-  __syncthreads();
-  for (int o = tid; o < a.k; o += kThreads) {
+  for (int i = tid; i < K * D; i += kThreads) {
+    const int o = i / D, e = i - (i / D) * D;
     const int dy = a.offs[2 * o];
-    const int lo = dy > 0 ? 0 : -dy, hi = dy > 0 ? H - dy : H;  // valid source rows [lo,hi)
+    const int lo = dy > 0 ? 0 : -dy, hi = dy > 0 ? H - dy : H;
     const int nrows = hi > lo ? hi - lo : 0;
+    double kk = (double)a.bk[e] * (double)nrows * (double)W;
+    for (int c = 0; c < C; ++c) kk += (double)a.wk[e * C + c] * sco[c * K + o];
+    kkb[i] = kk;
+  }
+  __syncthreads();
+  for (int o = tid; o < K; o += kThreads) {
     double L = 0.0;
-    for (int e = 0; e < a.d; ++e) {
-      double kk = (double)a.bk[e] * (double)nrows * (double)W;
-      for (int c = 0; c < C; ++c) {
-        double S = 0.0;
-        for (int r = lo; r < hi; ++r) S += rs[c * H + r];
-        kk += (double)a.wk[e * C + c] * S;
-      }
-      L += qbar[e] * (kk / (double)HW);
-    }
+    for (int e = 0; e < D; ++e) L += qbar[e] * (kkb[o * D + e] / (double)HW);
     logit[o] = L;
   }
   __syncthreads();
   if (tid == 0) {
     double mx = -INFINITY;
-    for (int o = 0; o < a.k; ++o) mx = fmax(mx, logit[o]);
+    for (int o = 0; o < K; ++o) mx = fmax(mx, logit[o]);
     const double T = fabs((double)a.scaling[0]) + 1e-6;
     double sum = 0.0;
-    for (int o = 0; o < a.k; ++o) {
+    for (int o = 0; o < K; ++o) {
       logit[o] = exp((logit[o] - mx) / T);
       sum += logit[o];
     }
-    for (int o = 0; o < a.k; ++o) a.offw[(size_t)b * a.k + o] = (float)(logit[o] / sum);
+    for (int o = 0; o < K; ++o) a.offw[(size_t)b * K + o] = (float)(logit[o] / sum);
   }
 }
 
@@ -1446,21 +1473,28 @@ struct Variant {
   const void* fold_fn[2];            // the same K1 that also finishes the previous step (rollouts) on the
                                      // [dense, compact] update field, or null
   int lds_fold;                      // the fold variant's LDS bytes
+  const void* fn_zp;                 // the zero-padded-shift instance (graph split K1s), or null
 };
 
-#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0, {nullptr, nullptr}, 0}
+template <int TH, int TW, int RY, int RX, int KU>
+constexpr const void* ks_zp_fn() {
+  if constexpr (KU > 0) return reinterpret_cast<const void*>(&gnca_k1_split<TH, TW, RY, RX, KU, 0, true>);
+  else return nullptr;
+}
+
+#define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0, {nullptr, nullptr}, 0, nullptr}
 #define GNCA_SV(th, tw, ry, rx, ku) \
   {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
-   ks_layout<th, tw, ry, rx>().total, {nullptr, nullptr}, 0}
+   ks_layout<th, tw, ry, rx>().total, {nullptr, nullptr}, 0, ks_zp_fn<th, tw, ry, rx, ku>()}
 // fold variants: the large-batch tile (dense: nullptr, it is only planned with the compact field) and
 // the small-batch ones (both layouts)
 #define GNCA_SVF(th, tw, ry, rx, ku, dense) \
   {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
    ks_layout<th, tw, ry, rx>().total, {dense, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku, 2>)}, \
-   ks_layout<th, tw, ry, rx, true>().total}
+   ks_layout<th, tw, ry, rx, true>().total, ks_zp_fn<th, tw, ry, rx, ku>()}
 #define GNCA_S32V(th, tw, ry, rx, ku) \
   {32, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split32<th, tw, ry, rx, ku>), 512, 2, \
-   ks32_layout<th, tw, ry, rx>().total, {nullptr, nullptr}, 0}
+   ks32_layout<th, tw, ry, rx>().total, {nullptr, nullptr}, 0, nullptr}
 static const Variant kVariants[] = {
     // 16 channels, hidden 128, bf16 MFMA on exact 3-way splits (gnca_k1_split.h), compile-time
     // geometry: list order is the large-batch preference (24x36: the largest tiles whose halo fits
@@ -1498,6 +1532,7 @@ static const Variant* find_variant(int C, int Hd) {
 
 struct Plan {
   const Variant* var;
+  const void* k1fn;   // the K1 launched: var->fn, or var->fn_zp for a zero-padded graph step
   int k, RY, RX, TH, TW, tiles_x, tiles_y, tps, total_tiles;
   int ppt;   // GroupNorm partial pairs per tile: one per K1 wave
   size_t lds1;
@@ -1558,7 +1593,8 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
       if (sscanf(tile_env, "%dx%d", &th, &tw) == 2 && (th != v.TH || tw != v.TW)) continue;
     }
     if (d->H % v.TH || d->W % v.TW || ry > v.RY || rx > v.RX) continue;
-    if (v.KU > 0 ? !(P->graph_on && !zp && !P->need_k0 && P->k == v.KU) : P->graph_on) continue;
+    // (zero-padded graph steps: the variant's ZP instance, fed K0's per-sample offset weights)
+    if (v.KU > 0 ? !(P->graph_on && P->k == v.KU && (!zp || v.fn_zp)) : P->graph_on) continue;
     if ((size_t)v.lds_split > (size_t)max_lds_bytes()) continue;
     // list order is the large-batch preference (big tiles amortise the per-tile work); a batch
     // too small to give every CU two workgroups' worth of tiles takes the variant with the most
@@ -1610,6 +1646,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->TH = bth;
   P->TW = btw;
   P->lds1 = blds;
+  P->k1fn = (zp && P->graph_on && P->var->fn_zp) ? P->var->fn_zp : P->var->fn;
   P->tiles_x = (d->W + btw - 1) / btw;
   P->tiles_y = (d->H + bth - 1) / bth;
   P->tps = P->tiles_x * P->tiles_y;
@@ -1686,7 +1723,8 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // region comes after the tile's groups and waits on its loads ("The fold").  Small
   // batches (dense field) fold: one launch per step instead of two (BASELINE c2 18.6 -> 15.7 us,
   // c3 20.4 -> 18.3 us).  A rollout asks for the compact fold with GNCA_ROLLOUT_FOLD (fold_any).
-  P->fold_any = P->var->fold_fn[P->compact_ok ? 1 : 0] != nullptr && !msg_only && !attn_on &&
+  // (not with K0: the zero-padded shift's offset weights come from the step's own finalized state)
+  P->fold_any = P->var->fold_fn[P->compact_ok ? 1 : 0] != nullptr && !msg_only && !attn_on && !P->need_k0 &&
                (P->graph_on ? P->k == P->var->KU : P->var->KU == 0) &&
                d->alpha_thr >= 0.f && d->graph_alpha_thr >= d->alpha_thr && n < (size_t)1 << 31 &&
                P->tps * P->ppt <= 256;
@@ -1821,13 +1859,16 @@ static int launch_k0(const gnca_step_desc* d, const gnca_weights* w, const Plan&
   k0.offw = reinterpret_cast<float*>(ws + P.off_offw);
   k0.B = d->B; k0.C = d->C; k0.H = d->H; k0.W = d->W; k0.d = d->d_model; k0.k = P.k;
   for (int o = 0; o < 2 * P.k; ++o) k0.offs[o] = d->offsets[o];
-  const size_t lds = ((size_t)d->C * d->H + d->C + d->d_model + P.k) * sizeof(double);
+  const size_t lds = ((size_t)d->C * d->H + d->C + d->d_model + P.k + (size_t)d->C * P.k +
+                      (size_t)P.k * d->d_model) * sizeof(double);
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gnca_k0_offset_weights),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(gnca_k0_offset_weights, dim3(d->B), dim3(kThreads), lds, st, k0);
   return check_launch();
 }
 
 static int launch_k1(const K1Args& k1, const Plan& P, hipStream_t st) {
-  const int occ = occupancy(P.var->fn, P.lds1, P.var->NT);
+  const int occ = occupancy(P.k1fn, P.lds1, P.var->NT);
   long grid = (long)device_cus() * occ;
   // measurement knob (A/B builds only): leave CUs free of K1 workgroups (for K2 of the other sub-batch)
   static const char* free_env = GNCA_AB_ENV("GNCA_K1_FREE_CUS");
@@ -1835,7 +1876,7 @@ static int launch_k1(const K1Args& k1, const Plan& P, hipStream_t st) {
   if (grid > P.total_tiles) grid = P.total_tiles;
   if (grid < 1) grid = 1;
   void* args[] = {const_cast<K1Args*>(&k1)};
-  const hipError_t e = hipLaunchKernel(P.var->fn, dim3((unsigned)grid), dim3(P.var->NT), args, P.lds1, st);
+  const hipError_t e = hipLaunchKernel(P.k1fn, dim3((unsigned)grid), dim3(P.var->NT), args, P.lds1, st);
   if (e != hipSuccess) {
     g_last_hip = (int)e;
     return GNCA_ERR_HIP;
@@ -1934,7 +1975,7 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   // measurement: K1's workgroups stamp into stamps[0 .. 2*cap), K2's into stamps[2*cap .. 4*cap)
   k1.stamps = stamps;
   k1.wimg = P.var->split == 1 ? wimg : nullptr;
-  if (stamps && (long)std::min<long>((long)device_cus() * occupancy(P.var->fn, P.lds1, P.var->NT),
+  if (stamps && (long)std::min<long>((long)device_cus() * occupancy(P.k1fn, P.lds1, P.var->NT),
                                      P.total_tiles) > stamp_cap)
     return GNCA_ERR_INVALID;
   if ((phases & GNCA_PHASE_K1) && (rc = launch_k1(k1, P, st)) != GNCA_OK) return rc;

@@ -43,11 +43,12 @@ CASES = {
                    "gnca_k1_split32<16,16,5,8,16>", True),
     # zero-pad mode (the ctor default, graph_augmentation.py:85-92: rows shifted with zero fill, the
     # column offset ignored; per-sample softmax offset weights from K0): the attention debugger's
-    # mode (test_graph_augmented_nca.py:284), on the fp32-MFMA runtime K1 that serves it
-    "graph_zeropad_f32": ("graph_zeropad_latest_grown_b1_72", True, 16, 72, 8, 4, 8, 96, (0, 7),
-                          "gnca_k1_update<16,128,0,0,0,0,0,256>", False, True),
+    # mode (test_graph_augmented_nca.py:284), on the split K1's zero-padded-shift instance (round 5;
+    # the fp32-MFMA runtime K1 before)
+    "graph_zeropad_split8x24": ("graph_zeropad_latest_grown_b1_72", True, 16, 72, 8, 4, 8, 96, (0, 7),
+                                "gnca_k1_split<8,24,4,4,8>", False, True),
 }
-ARITH = {"graph_zeropad_f32": "f32"}   # the others: bf16x6 (the split K1s)
+ARITH = {}   # every case: bf16x6 (the split K1s)
 # every case's max |hip - f64| is appended here (JSON lines; the GPU box merges gpurun_out/ back)
 DRIFT_LOG = os.environ.get("GNCA_DRIFT_LOG", os.path.join(os.path.dirname(os.path.dirname(
     os.path.abspath(__file__))), "gpurun_out", "drift_log.jsonl"))
