@@ -1381,6 +1381,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_dots(const BC2Args a) {
 // (Q and K enter only through their spatial means, so their x-gradient is constant per row).
 struct BDArgs {
   const float* x;
+  const double* rs;   // the forward K0's row sums of x ([B][C][H], fp64), or null: computed here
   const float* wq;
   const float* bq;
   const float* wk;
@@ -1407,16 +1408,19 @@ __global__ __launch_bounds__(kThreads) void gnca_b_attn(const BDArgs a) {
   double* gkp = gqp + d;                          // [k][d]
   double* gks = gkp + (size_t)k * d;              // [H][d]: sum of gkp over offsets valid for row
   double* sc = gks + (size_t)H * d;               // [2]: g_scaling, HW
+  float* wqs = reinterpret_cast<float*>(sc + 2);  // [d][C] W_Q, then W_K: LDS copies (the loops below read
+  float* wks = wqs + (size_t)d * C;               // them per channel / per unit, a global round trip each)
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t HW = (size_t)H * W;
   const float* xb = a.x + (size_t)b * C * HW;
-  for (int cr = wave; cr < C * H; cr += NW) {
-    const int c = cr / H, r = cr - c * H;
-    double s = 0.0;
-    for (int j = lane; j < W; j += 64) s += (double)xb[c * HW + (size_t)r * W + j];
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0) rs[cr] = s;
+  for (int e = tid; e < d * C; e += kThreads) {
+    wqs[e] = a.wq[e];
+    wks[e] = a.wk[e];
   }
+  if (a.rs)   // the forward's K0 row sums (the same x, the same bits)
+    for (int e = tid; e < C * H; e += kThreads) rs[e] = a.rs[(size_t)b * C * H + e];
+  else
+    row_sums_f64<8>(xb, C, H, W, rs, lane, wave, NW);
   __syncthreads();
   for (int c = tid; c < C; c += kThreads) {
     double s = 0.0;
@@ -1434,7 +1438,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_attn(const BDArgs a) {
   __syncthreads();
   for (int e = tid; e < d; e += kThreads) {
     double s = (double)a.bq[e];
-    for (int c = 0; c < C; ++c) s += (double)a.wq[e * C + c] * xbar[c];
+    for (int c = 0; c < C; ++c) s += (double)wqs[e * C + c] * xbar[c];
     qbar[e] = s;
   }
   for (int e = tid; e < k * d; e += kThreads) {
@@ -1443,7 +1447,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_attn(const BDArgs a) {
     const int lo = dy > 0 ? 0 : -dy, hi = dy > 0 ? H - dy : H;
     const double n_o = (double)(hi > lo ? hi - lo : 0) * (double)W;
     double s = (double)a.bk[j] * n_o;
-    for (int c = 0; c < C; ++c) s += (double)a.wk[j * C + c] * So[o * C + c];
+    for (int c = 0; c < C; ++c) s += (double)wks[j * C + c] * So[o * C + c];
     kb[e] = s / (double)HW;
   }
   __syncthreads();
@@ -1517,7 +1521,7 @@ __global__ __launch_bounds__(kThreads) void gnca_b_attn(const BDArgs a) {
   for (int e = tid; e < H * C; e += kThreads) {
     const int r = e / C, c = e - r * C;
     double s = 0.0;
-    for (int j = 0; j < d; ++j) s += (double)a.wq[j * C + c] * gqp[j] + (double)a.wk[j * C + c] * gks[r * d + j];
+    for (int j = 0; j < d; ++j) s += (double)wqs[j * C + c] * gqp[j] + (double)wks[j * C + c] * gks[r * d + j];
     a.corr[((size_t)b * H + r) * C + c] = (float)(s / (double)HW);
   }
 }
@@ -1822,7 +1826,7 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   P->nrb = (H + P->rows_per - 1) / P->rows_per;
   const int dm = std::max(d->d_model, 1), k = std::max(P->F.k, 1);
   P->ldsD = ((size_t)C * H + C + dm + (size_t)k * C + (size_t)k * dm + 2 * k + dm + (size_t)k * dm +
-             (size_t)H * dm + 2) * sizeof(double);
+             (size_t)H * dm + 2) * sizeof(double) + 2 * (size_t)dm * C * sizeof(float);
   if (P->msg && P->zp && P->ldsD > 64 * 1024) return false;
   P->o_w1 = 0;
   P->o_b1 = Hd * 3 * C;
@@ -2070,6 +2074,8 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     a.B = B; a.C = C; a.H = H; a.W = W; a.k = P.F.k; a.nrb = P.nrb; a.rows_per = P.rows_per;
     a.gthr = d.graph_alpha_thr; a.a2a = (d.flags & GNCA_ALIVE_TO_ALIVE) ? 1 : 0;
     for (int o = 0; o < 2 * P.F.k; ++o) a.offs[o] = d.offsets[o];
+    // (one workgroup per (sample, offset, row block); one per (sample, row block) with every offset's
+    //  sums in registers measured 3x slower at B=16 40^2: 156 vs 47 us, too few workgroups)
     hipLaunchKernelGGL(gnca_b_dots, dim3(B * P.F.k * P.nrb), dim3(kThreads), 0, st, a);
     if ((rc = bwd_check()) != GNCA_OK) return rc;
   }
@@ -2077,6 +2083,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     BDArgs a;
     memset(&a, 0, sizeof(a));
     a.x = x; a.wq = w->wq; a.bq = w->bq; a.wk = w->wk; a.bk = w->bk; a.scaling = w->scaling;
+    a.rs = reinterpret_cast<const double*>(fw + P.F.off_rs);
     a.dots = dots; a.pq = pq; a.corr = corr;
     a.B = B; a.C = C; a.H = H; a.W = W; a.d = d.d_model; a.k = P.F.k; a.nrb = P.nrb;
     for (int o = 0; o < 2 * P.F.k; ++o) a.offs[o] = d.offsets[o];

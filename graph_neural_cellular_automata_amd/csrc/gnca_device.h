@@ -90,6 +90,38 @@ __device__ __forceinline__ float fast_tanh(float x) {
 }
 
 __host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
+
+// Per (channel, row) fp64 sums of a sample's [C][H][W] plane set into rs[C*H]: one wave per row,
+// lanes striding the row, a fixed-order shuffle tree.  A wave takes U rows at a time with all their
+// loads in flight (one row per memory round trip made K0 0.45 ms at B=16 40^2); any U gives the
+// same bits (each row's sum is computed the same way).
+template <int U>
+__device__ __forceinline__ void row_sums_f64(const float* xb, int C, int H, int W, double* rs, int lane, int wave,
+                                             int nwaves) {
+  const size_t HW = (size_t)H * W;
+  for (int base = wave * U; base < C * H; base += nwaves * U) {
+    double s[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s[u] = 0.0;
+    for (int j = lane; j < W; j += 64) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int cr = base + u;
+        v[u] = cr < C * H ? xb[(size_t)(cr / H) * HW + (size_t)(cr - (cr / H) * H) * W + j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) s[u] += (double)v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      for (int off = 32; off > 0; off >>= 1) s[u] += __shfl_xor(s[u], off);
+    if (lane == 0)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (base + u < C * H) rs[base + u] = s[u];
+  }
+}
 __host__ __device__ constexpr int odd4(int v) {  // round up to 4*odd: conflict-free 16-lane b128
   return ((((v + 3) & ~3) >> 2) & 1) ? ((v + 3) & ~3) : ((v + 3) & ~3) + 4;
 }
@@ -215,6 +247,7 @@ __device__ __forceinline__ void wave_sum2_regs(const double (&a)[4], const doubl
 // the backward recomputes them there.
 struct FwdLayout {
   size_t ws_bytes, off_dx, off_stats, off_offw;
+  size_t off_rs;   // K0's per-(channel, row) fp64 sums of x (zero-pad mode), for the backward's BD
   int tps, k;
   bool graph_on, need_k0;
 };

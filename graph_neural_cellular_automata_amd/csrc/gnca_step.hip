@@ -1330,9 +1330,18 @@ struct K0Args {
   const float* bk;
   const float* scaling;
   float* offw;  // [B * k]
+  const double* rs;   // [B][C][H] per-row channel sums (gnca_k0_rowsums)
   int B, C, H, W, d, k;
   int8_t offs[2 * GNCA_MAX_OFFSETS];
 };
+
+// K0's first phase: the per-(channel, row) fp64 sums of x, one workgroup per (channel, sample) so that
+// a small batch still spreads over the chip (one workgroup per sample took 57 us for B=16 40^2)
+__global__ __launch_bounds__(kThreads) void gnca_k0_rowsums(const float* x, double* rs, int C, int H, int W) {
+  const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t HW = (size_t)H * W;
+  row_sums_f64<4>(x + ((size_t)b * C + c) * HW, 1, H, W, rs + ((size_t)b * C + c) * H, lane, wave, kThreads / 64);
+}
 
 __global__ __launch_bounds__(kThreads) void gnca_k0_offset_weights(const K0Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1343,36 +1352,20 @@ __global__ __launch_bounds__(kThreads) void gnca_k0_offset_weights(const K0Args 
   double* logit = qbar + D;                              // [k]
   double* sco = logit + K;                               // [C][k] sum of a channel's rows an offset keeps
   double* kkb = sco + (size_t)C * K;                     // [k][d] pooled key of each offset
+  float* wqs = reinterpret_cast<float*>(kkb + (size_t)K * D);   // [d][C] W_Q, then [d][C] W_K (LDS copies:
+  float* wks = wqs + (size_t)D * C;                             //  the dot products' loops read them per c)
   const int b = blockIdx.x, tid = threadIdx.x;
   const size_t HW = (size_t)H * W;
   const float* xb = a.x + (size_t)b * C * HW;
   const int lane = tid & 63, wave = tid >> 6;
-  // row sums: one wave per (c, row), lanes stride the row, fixed-order shuffle tree; a wave takes
-  // U rows at a time with all their loads in flight (one row at a time paid a memory round trip
-  // per row: 0.45 ms for B=16 40^2); the same sums bit for bit
-  constexpr int U = 8;
-  for (int base = wave * U; base < C * H; base += (kThreads / 64) * U) {
-    double s[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) s[u] = 0.0;
-    for (int j = lane; j < W; j += 64) {
-      float v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int cr = base + u;
-        v[u] = cr < C * H ? xb[(size_t)(cr / H) * HW + (size_t)(cr - (cr / H) * H) * W + j] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) s[u] += (double)v[u];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      for (int off = 32; off > 0; off >>= 1) s[u] += __shfl_xor(s[u], off);
-    if (lane == 0)
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (base + u < C * H) rs[base + u] = s[u];
+  // the projection weights and the sample's row sums (gnca_k0_rowsums, one workgroup per (sample,
+  // channel) before this launch) to LDS, every load in flight
+  (void)xb; (void)lane; (void)wave;
+  for (int e = tid; e < D * C; e += kThreads) {
+    wqs[e] = a.wq[e];
+    wks[e] = a.wk[e];
   }
+  for (int e = tid; e < C * H; e += kThreads) rs[e] = a.rs[(size_t)b * C * H + e];
   __syncthreads();
   // channel means; per (channel, offset) the sum of the rows the zero-padded shift keeps
   for (int c = tid; c < C; c += kThreads) {
@@ -1391,7 +1384,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k0_offset_weights(const K0Args 
   __syncthreads();
   for (int e = tid; e < D; e += kThreads) {
     double s = (double)a.bq[e];
-    for (int c = 0; c < C; ++c) s += (double)a.wq[e * C + c] * xbar[c];
+    for (int c = 0; c < C; ++c) s += (double)wqs[e * C + c] * xbar[c];
     qbar[e] = s;
   }
   for (int i = tid; i < K * D; i += kThreads) {
@@ -1400,7 +1393,7 @@ __global__ __launch_bounds__(kThreads) void gnca_k0_offset_weights(const K0Args 
     const int lo = dy > 0 ? 0 : -dy, hi = dy > 0 ? H - dy : H;
     const int nrows = hi > lo ? hi - lo : 0;
     double kk = (double)a.bk[e] * (double)nrows * (double)W;
-    for (int c = 0; c < C; ++c) kk += (double)a.wk[e * C + c] * sco[c * K + o];
+    for (int c = 0; c < C; ++c) kk += (double)wks[e * C + c] * sco[c * K + o];
     kkb[i] = kk;
   }
   __syncthreads();
@@ -1543,7 +1536,7 @@ struct Plan {
   int band_c, nbands_c, total2_c;   // K2 on the compact update field
   size_t lds2_c;
   // workspace carve (bytes)
-  size_t off_dx, off_stats, off_mm, off_offw, off_alive, off_rmask, off_rpre, off_dxa, off_wimg, ws_bytes;
+  size_t off_dx, off_stats, off_mm, off_offw, off_rs, off_alive, off_rmask, off_rpre, off_dxa, off_wimg, ws_bytes;
   bool compact_ok;   // the rollout's compact update field (the bf16-split K1s, large batches)
   // the fold (rollouts of a fold-capable K1 on the compact field): K1 of step t also finishes step
   // t - 1, so the compact field (dx, row tables, alpha plane, partials) is double-buffered by the
@@ -1682,6 +1675,7 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->off_stats = carve((size_t)P->total_tiles * P->ppt * 2 * sizeof(double));
   P->off_mm = carve((size_t)P->total_tiles * 2 * sizeof(float));
   P->off_offw = carve((size_t)d->B * (P->k > 0 ? P->k : 1) * sizeof(float));
+  P->off_rs = carve(P->need_k0 ? (size_t)d->B * d->C * d->H * sizeof(double) : 0);   // K0's row sums
   P->off_alive = carve((size_t)d->B * d->H * d->W);   // rollout: K2 -> next K1 alive bytes
   // rollout: the compact update field's per-tile-row live masks and prefixes (split K1)
   // (large batches only: a small batch's K2 needs thin bands to fill the chip, where unpacking the
@@ -1761,6 +1755,7 @@ bool fwd_layout(const gnca_step_desc* d, FwdLayout* out) {
   out->off_dx = P.off_dx;
   out->off_stats = P.off_stats;
   out->off_offw = P.off_offw;
+  out->off_rs = P.off_rs;
   out->tps = P.tps * P.ppt;   // GroupNorm partial pairs per sample
   out->k = P.k;
   out->graph_on = P.graph_on;
@@ -1857,10 +1852,14 @@ static int launch_k0(const gnca_step_desc* d, const gnca_weights* w, const Plan&
   memset(&k0, 0, sizeof(k0));
   k0.x = x; k0.wq = w->wq; k0.bq = w->bq; k0.wk = w->wk; k0.bk = w->bk; k0.scaling = w->scaling;
   k0.offw = reinterpret_cast<float*>(ws + P.off_offw);
+  double* rs = reinterpret_cast<double*>(ws + P.off_rs);
+  k0.rs = rs;
   k0.B = d->B; k0.C = d->C; k0.H = d->H; k0.W = d->W; k0.d = d->d_model; k0.k = P.k;
+  if (d->B > 65535) return GNCA_ERR_UNSUPPORTED;   // (grid y)
+  hipLaunchKernelGGL(gnca_k0_rowsums, dim3(d->C, d->B), dim3(kThreads), 0, st, x, rs, d->C, d->H, d->W);
   for (int o = 0; o < 2 * P.k; ++o) k0.offs[o] = d->offsets[o];
   const size_t lds = ((size_t)d->C * d->H + d->C + d->d_model + P.k + (size_t)d->C * P.k +
-                      (size_t)P.k * d->d_model) * sizeof(double);
+                      (size_t)P.k * d->d_model) * sizeof(double) + 2 * (size_t)d->d_model * d->C * sizeof(float);
   if (lds > 64 * 1024) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gnca_k0_offset_weights),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(gnca_k0_offset_weights, dim3(d->B), dim3(kThreads), lds, st, k0);
