@@ -57,6 +57,10 @@ WORKLOADS = {
                name="classic NCA rollout (BASELINE config 2), fire 0.5"),
     "c3": dict(graph=True, C=16, H=72, B=8, R=4, K=8, fixture="graph_torus_latest_grown_b1_72",
                name="graph-augmented NCA rollout (BASELINE config 3), torus, r=4, K=8, fire 0.5"),
+    # the module's default shift (graph_augmentation.py:42 zero_padded_shift=True; the attention
+    # debugger's mode): per-sample softmax offset weights (K0) every step, rows shifted with zero fill
+    "zeropad": dict(graph=True, zp=True, C=16, H=72, B=1024, R=4, K=8, fixture="graph_zeropad_latest_grown_b1_72",
+                    name="graph-augmented NCA rollout, zero-padded shift (the module default), r=4, K=8, fire 0.5"),
     "c5": dict(graph=True, C=32, H=128, B=128, R=5, K=16, fixture="graph_torus_c32_r5_k16_b1_48",
                name="graph-augmented NCA rollout (BASELINE config 5), 32ch, torus, r=5, K=16, "
                     "fire 0.5, pool 1024 sharded 128/GPU"),
@@ -157,6 +161,8 @@ def make_desc(wl, B, H, W, offsets, rank, step0=0):
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
     flags = L.USE_GROUPNORM | ((L.GRAPH | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE) if wl["graph"] else 0)
+    if wl.get("zp"):
+        flags |= L.ZERO_PAD_SHIFT
     return S.make_desc(B=B, C=wl["C"], H=H, W=W, hidden=HD, d_model=D_MODEL,
                        offsets=offsets if wl["graph"] else [], flags=flags,
                        update_gain=GAIN, alpha_thr=THR, message_gain=MSG_GAIN, fire_rate=FIRE,
@@ -753,7 +759,7 @@ def main():
     ph = L.PHASE_COMPACT if compact else 0
 
     def launch(t, src, dst, which):
-        f = (L.PHASE_K1 | (L.PHASE_ALIVE if t > 0 else 0)) if which == 1 else (L.PHASE_K2 | L.PHASE_ALIVE)
+        f = (L.PHASE_K0 | L.PHASE_K1 | (L.PHASE_ALIVE if t > 0 else 0)) if which == 1 else (L.PHASE_K2 | L.PHASE_ALIVE)
         L.check(lib.gnca_step_phases_f32(ctypes.byref(descs[t]), ctypes.byref(w), src.data_ptr(),
                                          dst.data_ptr(), None, None, ws.data_ptr(), ws.numel(), sptr,
                                          f | ph), f"k{which}")
