@@ -1565,21 +1565,35 @@ __global__ __launch_bounds__(kThreads) void gnca_b_reduce(const RedArgs a) {
   const int begin = s == 0 ? 0 : a.end[s - 1];
   const long src = a.col0[s] + (long)(col - begin) * a.step[s];
   double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+  // U steps of 4 rows (rows r + 16 i, i < 4U): every load in flight before the adds, which keep the
+  // one-step order (t0..t3 take rows r, r + 16, r + 32, r + 48 of each step), so the sums are the
+  // same bits as one step at a time, in ceil(rows / 64U) memory latencies instead of rows / 64
+  // (B=16 40^2: 960 rows, 15 dependent round trips per thread before)
+  auto steps = [&](auto U_, const auto* p, long& r) {
+    constexpr int U = decltype(U_)::value;
+    for (; r + 64 * (U - 1) + 48 < a.rows; r += 64 * U) {
+      double v[4 * U];
+#pragma unroll
+      for (int i = 0; i < 4 * U; ++i) v[i] = (double)p[(r + 16 * i) * a.stride];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        t0 += v[4 * u]; t1 += v[4 * u + 1]; t2 += v[4 * u + 2]; t3 += v[4 * u + 3];
+      }
+    }
+  };
   if (col < a.ncols && a.step[s] != 0) {
     long r = rg;
     if (a.f64) {
       const double* p = reinterpret_cast<const double*>(a.part) + src;
-      for (; r + 48 < a.rows; r += 64) {
-        t0 += p[r * a.stride]; t1 += p[(r + 16) * a.stride];
-        t2 += p[(r + 32) * a.stride]; t3 += p[(r + 48) * a.stride];
-      }
+      steps(std::integral_constant<int, 8>{}, p, r);
+      steps(std::integral_constant<int, 2>{}, p, r);
+      steps(std::integral_constant<int, 1>{}, p, r);
       for (; r < a.rows; r += 16) t0 += p[r * a.stride];
     } else {
       const float* p = reinterpret_cast<const float*>(a.part) + src;
-      for (; r + 48 < a.rows; r += 64) {
-        t0 += (double)p[r * a.stride]; t1 += (double)p[(r + 16) * a.stride];
-        t2 += (double)p[(r + 32) * a.stride]; t3 += (double)p[(r + 48) * a.stride];
-      }
+      steps(std::integral_constant<int, 8>{}, p, r);
+      steps(std::integral_constant<int, 2>{}, p, r);
+      steps(std::integral_constant<int, 1>{}, p, r);
       for (; r < a.rows; r += 16) t0 += (double)p[r * a.stride];
     }
   }
@@ -1886,6 +1900,64 @@ struct Reducer {
   }
 };
 
+// The weight-gradient reductions depend only on BB's and BA's partial rows, not on BC: they run on a
+// per-device side stream beside BC (forked from the caller's stream after BB, joined back before
+// the entry point returns, so every later use of the outputs and workspace on the caller's stream
+// is ordered after them).  Created once per device, never destroyed (as the rollout's sub-streams).
+struct BwdSide {
+  hipStream_t s;
+  hipEvent_t fork, join;
+  std::mutex mu;   // one backward's fork .. join enqueue at a time per device
+};
+
+static BwdSide* bwd_side() {
+  static std::mutex mu;
+  static std::unordered_map<int, BwdSide*> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  BwdSide* bs = new BwdSide();
+  if (hipStreamCreateWithFlags(&bs->s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&bs->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&bs->join, hipEventDisableTiming) != hipSuccess)
+    return nullptr;
+  cache[dev] = bs;
+  return bs;
+}
+
+// Fork on construction, join on destruction (every return path of the backward, errors included);
+// without a side stream (or GNCA_BWD_ONE_STREAM in A/B builds) everything stays on the caller's.
+// Only for large steps: the fork and join cost a small, host-bound backward more than the overlap
+// gives (B=16 40^2: 0.092 -> 0.103 ms; B=128 72^2: 0.623 -> 0.608; B=1024: equal)
+constexpr long kSideMinCells = 1L << 19;
+struct SideFork {
+  hipStream_t main, side;
+  BwdSide* bs = nullptr;
+  std::unique_lock<std::mutex> lk;
+  bool ok = true;
+  SideFork(hipStream_t st, long cells) : main(st), side(st) {
+#ifndef GNCA_BWD_ONE_STREAM
+    if (cells < kSideMinCells) return;
+    bs = bwd_side();
+    if (!bs) return;
+    lk = std::unique_lock<std::mutex>(bs->mu);
+    if (hipEventRecord(bs->fork, st) != hipSuccess || hipStreamWaitEvent(bs->s, bs->fork, 0) != hipSuccess) {
+      ok = false;
+      return;
+    }
+    side = bs->s;
+#endif
+  }
+  ~SideFork() {
+    if (side != main) {
+      (void)hipEventRecord(bs->join, side);
+      (void)hipStreamWaitEvent(main, bs->join, 0);
+    }
+  }
+};
+
 
 }  // namespace
 }  // namespace gnca
@@ -2013,6 +2085,34 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
       if ((rc = bwd_check()) != GNCA_OK) return rc;
     }
   }
+  // the weight-gradient reductions (BB's and BA's partial rows) on the side stream, beside BC
+  SideFork sf(st, (long)B * (long)HW);
+  if (!sf.ok) return GNCA_ERR_HIP;
+  const int dmod = std::max(d.d_model, 1);
+  {
+    Reducer r(pb, false, (long)P.gridB * NW, P.npart);
+    r.add(P.o_w1, Hd * 3 * C, 1, grads->w1);
+    r.add(P.o_b1, Hd, 1, grads->b1);
+    r.add(P.o_w2, C * Hd, 1, grads->w2);
+    if (P.graph) {
+      r.add(P.o_wm, C * C, 1, grads->wm);
+      r.add(P.o_bm, C, 1, grads->bm);
+      if (!(P.msg && P.zp)) {   // torus (or no message): the offset weights are constants
+        r.add(0, dmod * C, 0, grads->wq);
+        r.add(0, dmod, 0, grads->bq);
+        r.add(0, dmod * C, 0, grads->wk);
+        r.add(0, dmod, 0, grads->bk);
+        r.add(0, 1, 0, grads->scaling);
+      }
+    }
+    if ((rc = r.launch(sf.side)) != GNCA_OK) return rc;
+  }
+  if (P.gn) {
+    Reducer r(pa, true, (long)B * P.nbands, 2 + 2 * C);
+    r.add(2, C, 2, grads->gn_weight);
+    r.add(3, C, 2, grads->gn_bias);
+    if ((rc = r.launch(sf.side)) != GNCA_OK) return rc;
+  }
   // BC
   {
     BCArgs a;
@@ -2037,31 +2137,6 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     for (int o = 0; o < 2 * a.k; ++o) a.offs[o] = d.offsets[o];
     hipLaunchKernelGGL(gnca_b_adjoint, dim3(B * P.tps3 * a.ncg), dim3(kThreads), P.ldsC, st, a);
     if ((rc = bwd_check()) != GNCA_OK) return rc;
-  }
-  const int dmod = std::max(d.d_model, 1);
-  {
-    Reducer r(pb, false, (long)P.gridB * NW, P.npart);
-    r.add(P.o_w1, Hd * 3 * C, 1, grads->w1);
-    r.add(P.o_b1, Hd, 1, grads->b1);
-    r.add(P.o_w2, C * Hd, 1, grads->w2);
-    if (P.graph) {
-      r.add(P.o_wm, C * C, 1, grads->wm);
-      r.add(P.o_bm, C, 1, grads->bm);
-      if (!(P.msg && P.zp)) {   // torus (or no message): the offset weights are constants
-        r.add(0, dmod * C, 0, grads->wq);
-        r.add(0, dmod, 0, grads->bq);
-        r.add(0, dmod * C, 0, grads->wk);
-        r.add(0, dmod, 0, grads->bk);
-        r.add(0, 1, 0, grads->scaling);
-      }
-    }
-    if ((rc = r.launch(st)) != GNCA_OK) return rc;
-  }
-  if (P.gn) {
-    Reducer r(pa, true, (long)B * P.nbands, 2 + 2 * C);
-    r.add(2, C, 2, grads->gn_weight);
-    r.add(3, C, 2, grads->gn_bias);
-    if ((rc = r.launch(st)) != GNCA_OK) return rc;
   }
   if (!P.graph || !(P.msg && P.zp)) return GNCA_OK;
   double* dots = reinterpret_cast<double*>(wsb + P.off_dots);
