@@ -84,6 +84,24 @@ def test_relu_keeps_nan_like_torch(dev):
     np.testing.assert_array_equal(np.isnan(out.cpu().numpy()), np.isnan(ref))
 
 
+@pytest.mark.parametrize("shape", [(0, 16, 40, 40), (2, 16, 0, 40)])
+def test_empty_state_raises_like_reference(dev, shape):
+    """The reference raises RuntimeError on an empty batch (its perception's reshape) and on an
+    empty canvas (conv2d's kernel larger than the padded input); its trainer skips empty masks
+    (train_graph_augmented_nca.py:305-307).  The module raises a RuntimeError too, launching
+    nothing."""
+    m = _trained_like(dev)
+    x = torch.zeros(shape, device=dev)
+    for kw in ({}, {"return_attention": True}):
+        with pytest.raises(RuntimeError):
+            with torch.no_grad():
+                m(x, fire_rate=0.5, **kw)
+    torch.cuda.synchronize()
+    # the device is still usable afterwards
+    with torch.no_grad():
+        assert torch.isfinite(m(_state(1, 16, 24, 24, dev), fire_rate=0.5)).all()
+
+
 def test_torch_rng_consumed_only_when_fire_rate_below_one(dev):
     m = _trained_like(dev)
     x = _state(1, 16, 24, 24, dev)
