@@ -81,24 +81,34 @@ def flop_per_cell(wl):
     return 2 * (3 * C * HD + HD * C + (C * C if wl["graph"] else 0))
 
 
-def pmc_traffic(kernel):
+def pmc_file(config):
+    """The committed PMC passes of ``config``: the headline's PMC_TRAFFIC, the other configs'
+    profiles/r05_pmc_traffic_<config>.json (tools/pmc.sh with BENCH_ARGS="--config <config>"), or None."""
+    if config == "headline":
+        return PMC_TRAFFIC
+    f = os.path.join(ROOT, "profiles", f"r05_pmc_traffic_{config}.json")
+    return f if os.path.exists(f) else None
+
+
+def pmc_traffic(kernel, config="headline"):
     """HBM bytes per STEP of ``kernel`` from the committed PMC passes: per-launch counter bytes x the
     launches per step the passes ran with (sub-batches; rollout kernels of 2 half-batches)."""
     try:
-        d = json.load(open(PMC_TRAFFIC))
+        d = json.load(open(pmc_file(config)))
         return d["kernels"][kernel]["traffic_bytes"] * d.get("launches_per_step", 1)
     except Exception:
         return None
 
 
-def pmc_mfma_busy(kernel, cus):
-    """MFMA pipe busy fraction of ``kernel`` from the committed PMC pass (profiles/*_pmc_traffic.json):
+def pmc_mfma_busy(kernel, cus, config="headline"):
+    """MFMA pipe busy fraction of ``kernel`` from the committed PMC pass (profiles/*_pmc_traffic*.json):
     SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over every SIMD: 32 per v_mfma_f32_32x32x16_bf16) /
     (GRBM_GUI_ACTIVE / 8 XCDs = the kernel's cycles, x 4 SIMDs x CUs)."""
     try:
-        c = json.load(open(PMC_TRAFFIC))["kernels"][kernel]["counters"]
+        f = pmc_file(config)
+        c = json.load(open(f))["kernels"][kernel]["counters"]
         busy, grbm = c["SQ_VALU_MFMA_BUSY_CYCLES"], c["GRBM_GUI_ACTIVE"]
-        return {"value": busy / (grbm / 8 * 4 * cus), "source": os.path.relpath(PMC_TRAFFIC, ROOT),
+        return {"value": busy / (grbm / 8 * 4 * cus), "source": os.path.relpath(f, ROOT),
                 "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 4 SIMDs x CUs)"}
     except Exception:
         return None
@@ -792,7 +802,6 @@ def main():
     # read x, write x'; read dx: dense NCHW, or on the compact field the alpha channel's dense
     # plane and the other channels' live values only
     k2_bytes = cells * 4 * (2 * C + (1 + (C - 1) * live_frac if compact else C))
-    headline = args.config == "headline"
     # executed MFMA work per launch: live cells are packed into groups of 32 per tile (split K1,
     # v_mfma_f32_32x32x16_bf16 of 32,768 FLOP each per group: 16 channels 108 + 4 for the message,
     # 32 channels 196 + 12; a tile's last group is padded) or, for the f32 K1, the FLOPs per live cell
@@ -809,8 +818,9 @@ def main():
     k1_s = k1_ms * 1e-3
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     k1_key = "K1F" if fold else "K1"      # the PMC passes' name for the timed K1 (tools/pmc_traffic.py)
-    pmc_busy = pmc_mfma_busy(k1_key, cus) if headline else None
-    k1_traffic = pmc_traffic(k1_key) if headline else None
+    pmc_busy = pmc_mfma_busy(k1_key, cus, args.config)
+    k1_traffic = pmc_traffic(k1_key, args.config)
+    pmc_src = pmc_file(args.config)
     roof = {"bound": "mfma", "kernel": k1_name[:-1] + ",fold>" if fold else k1_name, "arith": arith,
             "achieved": live_flops / k1_s / 1e12,
             "peak": peak_eq / 1e12, "unit": "TFLOP/s",
@@ -823,8 +833,8 @@ def main():
             "dense_flop_per_launch": dense_flops, "live_flop_per_launch": live_flops,
             "live_fraction": live_frac,
             "traffic": k1_traffic,
-            "traffic_unit": f"HBM bytes per step (2*FETCH_SIZE+WRITE_SIZE summed over the step's K1 "
-                            f"launches, {os.path.relpath(PMC_TRAFFIC, ROOT)})",
+            "traffic_unit": (f"HBM bytes per step (2*FETCH_SIZE+WRITE_SIZE summed over the step's K1 "
+                             f"launches, {os.path.relpath(pmc_src, ROOT)})") if pmc_src else None,
             # north_star's "HBM on the fused Sobel+gather stage": that stage is inside K1, which is
             # bound by its MFMA/VALU work (132+ FLOP per byte against the ridge's ~20), so its HBM
             # rate is reported, not targeted
@@ -847,7 +857,7 @@ def main():
                "k2_launches_timed": 1 if fold else launches * nsub,
                "note": ("the fold: K2 runs once per rollout (after its last step); every other step's "
                         "finish is inside the next step's K1") if fold else None,
-               "traffic": pmc_traffic("K2") if headline else None}
+               "traffic": pmc_traffic("K2", args.config)}
 
     if rank == 0:
         cpu = None

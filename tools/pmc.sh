@@ -9,10 +9,12 @@ ARGS="${PMC_CMD:-python3 bench.py --steps 4 --warmup 1 --no-cpu ${BENCH_ARGS:-}}
 REGEX="${PMC_REGEX:-gnca_k}"
 OUT="${PMC_OUT:-gpurun_out/pmc}"
 mkdir -p "$OUT"
+# PMC_PASSES: the pass numbers to run (default every pass), e.g. "1 2 4"
 i=0
 while read -r counters; do
   [ -z "$counters" ] && continue
   i=$((i+1))
+  if [ -n "${PMC_PASSES:-}" ] && ! [[ " $PMC_PASSES " == *" $i "* ]]; then continue; fi
   echo "=== pass $i: $counters"
   timeout -k 10 300 rocprofv3 --pmc $counters --kernel-include-regex "$REGEX" -d $OUT/p$i -o run --output-format csv -- $ARGS > $OUT/p$i.log 2>&1
   rc=$?

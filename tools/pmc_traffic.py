@@ -21,7 +21,9 @@ vals = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
 for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        k = ("K1F" if re.search(r", (true|1|2)>", k) else "K1") if "gnca_k1" in k else ("K2" if "k2_finalize" in k else None)
+        # the fold instances: gnca_k1_split's 6th template argument (FOLD) is 1 or 2
+        fold = re.search(r"gnca_k1_split<\d+, \d+, \d+, \d+, \d+, ([12])\b", k)
+        k = ("K1F" if fold else "K1") if "gnca_k1" in k else ("K2" if "k2_finalize" in k else None)
         if k:
             vals[k][r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
 res = {"fetch_correction": 2.0,
