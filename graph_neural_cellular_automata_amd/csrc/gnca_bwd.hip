@@ -1419,8 +1419,10 @@ __global__ __launch_bounds__(kThreads) void gnca_b_attn(const BDArgs a) {
   }
   if (a.rs)   // the forward's K0 row sums (the same x, the same bits)
     for (int e = tid; e < C * H; e += kThreads) rs[e] = a.rs[(size_t)b * C * H + e];
+  else if ((W & 3) == 0)
+    canon_row_sums<4, 2>(xb, C * H, W, rs, tid >> 5, kThreads / 32, tid & 31);
   else
-    row_sums_f64<8>(xb, C, H, W, rs, lane, wave, NW);
+    canon_row_sums<1, 2>(xb, C * H, W, rs, tid >> 5, kThreads / 32, tid & 31);
   __syncthreads();
   for (int c = tid; c < C; c += kThreads) {
     double s = 0.0;

@@ -91,35 +91,60 @@ __device__ __forceinline__ float fast_tanh(float x) {
 
 __host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
 
-// Per (channel, row) fp64 sums of a sample's [C][H][W] plane set into rs[C*H]: one wave per row,
-// lanes striding the row, a fixed-order shuffle tree.  A wave takes U rows at a time with all their
-// loads in flight (one row per memory round trip made K0 0.45 ms at B=16 40^2); any U gives the
-// same bits (each row's sum is computed the same way).
-template <int U>
-__device__ __forceinline__ void row_sums_f64(const float* xb, int C, int H, int W, double* rs, int lane, int wave,
-                                             int nwaves) {
-  const size_t HW = (size_t)H * W;
-  for (int base = wave * U; base < C * H; base += nwaves * U) {
-    double s[U];
+// The zero-padded shift's per (channel, row) fp64 sums of x (K0's pooled logits, BD), in ONE
+// canonical order that every producer follows, so that K2's fused sums (a rollout's next step) and
+// K0's own pass (single steps, a rollout's first step) give the same bits:
+//  * the row's cells in vectors of V = 4 (W % 4 == 0) or 1; P_k = ((v0 + v1) + (v2 + v3)) in fp64
+//    (V = 4) or v0;
+//  * 32 consecutive vectors per segment, lane k of a 32-lane half-wave holding P_k (+0.0 past the
+//    row's end), summed by an xor butterfly (16, 8, 4, 2, 1);
+//  * the segments' sums added in order (the first one as is).
+template <int V>
+__device__ __forceinline__ double canon_vec_sum(const float* v) {
+  if constexpr (V == 4) return ((double)v[0] + (double)v[1]) + ((double)v[2] + (double)v[3]);
+  else return (double)v[0];
+}
+
+// every lane of the wave calls it (the shuffles); the 32-lane half-waves reduce independently
+__device__ __forceinline__ double canon_butterfly32(double p) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) s[u] = 0.0;
-    for (int j = lane; j < W; j += 64) {
-      float v[U];
+  for (int off = 16; off > 0; off >>= 1) p += __shfl_xor(p, off);
+  return p;
+}
+
+// rows r = h, h + nh, ... of the [n_rows][W] planes at x (row r at x + r * W) into rs[r]: half-wave h
+// of nh, lane k = lane & 31.  U rows per half-wave in flight.  Every lane of the calling waves calls it.
+template <int V, int U>
+__device__ __forceinline__ void canon_row_sums(const float* x, int n_rows, int W, double* rs, int h, int nh, int k) {
+  typedef float vf __attribute__((ext_vector_type(V)));
+  const int nvr = W / V;
+  for (int r0 = 0; r0 < n_rows; r0 += U * nh) {   // uniform over the workgroup
+    double S[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) S[u] = 0.0;
+    for (int s0 = 0; s0 < nvr; s0 += 32) {
+      vf v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int cr = base + u;
-        v[u] = cr < C * H ? xb[(size_t)(cr / H) * HW + (size_t)(cr - (cr / H) * H) * W + j] : 0.f;
+        const int r = r0 + u * nh + h, q = s0 + k;
+        if (r < n_rows && q < nvr) v[u] = *reinterpret_cast<const vf*>(x + (size_t)r * W + (size_t)V * q);
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) s[u] += (double)v[u];
+      for (int u = 0; u < U; ++u) {
+        const int r = r0 + u * nh + h, q = s0 + k;
+        float f[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) f[i] = v[u][i];
+        const double p = canon_butterfly32((r < n_rows && q < nvr) ? canon_vec_sum<V>(f) : 0.0);
+        S[u] = s0 == 0 ? p : S[u] + p;
+      }
     }
+    if (k == 0)
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      for (int off = 32; off > 0; off >>= 1) s[u] += __shfl_xor(s[u], off);
-    if (lane == 0)
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (base + u < C * H) rs[base + u] = s[u];
+      for (int u = 0; u < U; ++u) {
+        const int r = r0 + u * nh + h;
+        if (r < n_rows) rs[r] = S[u];
+      }
   }
 }
 __host__ __device__ constexpr int odd4(int v) {  // round up to 4*odd: conflict-free 16-lane b128

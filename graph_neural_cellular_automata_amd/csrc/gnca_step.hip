@@ -946,6 +946,9 @@ struct K2Args {
   const float* dxa;        // [B,H,W] alpha-channel update of the live cells (K1Args::dxa)
   int TH, TW, tiles_x;
   uint64_t* stamps;        // measurement only (K1Args::stamps)
+  // zero-padded-shift rollouts on the compact field: the new state's per (channel, row) fp64 sums
+  // ([B][C][H], canon_row_sums' order) for the next step's K0, or null
+  double* rs;
 };
 
 // K2's sample for block-row j.  zigzag: K1 sweeps 8 contiguous sample ranges (one per XCD group)
@@ -971,8 +974,14 @@ __device__ __forceinline__ int k2_sample(int j, int B, int zigzag) {
 #ifndef GNCA_K2_CU_ALONE
 #define GNCA_K2_CU_ALONE 2
 #endif
+#ifndef GNCA_K2_CU_ROWS
+#define GNCA_K2_CU_ROWS 1   // the row-sum instance (ROWS below): 1 keeps it at 64 VGPRs (2: 67)
+#endif
 // CU: channels in flight per thread of the compact field's main pass (below)
-template <int V, bool COMPACT, int CU>
+// ROWS: the zero-padded-shift rollout's instance that also writes the new state's row sums (K2Args::rs;
+// its own instance, launched with one channel in flight: the fused sums' registers would lift the
+// plain one above the 64 VGPRs that let two K2 waves share a SIMD with the sub-batch pipeline's K1)
+template <int V, bool COMPACT, int CU, bool ROWS>
 __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_norm) {
   typedef float vf __attribute__((ext_vector_type(V)));
 #ifndef GNCA_K2_KU
@@ -1138,11 +1147,77 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
       *reinterpret_cast<vf*>(ob + p) = v;
     }
   };
+  typedef float vfu __attribute__((ext_vector_type(V), aligned(4)));
   if (!compact) {
     store_items(tid);
     for (int it0 = tid + KU * kThreads; it0 < nitems; it0 += KU * kThreads) {
       load_items(it0, true, true);
       store_items(it0);
+    }
+  } else if constexpr (ROWS) {
+    // zero-padded-shift rollouts: the compact pass below with the new state's row sums fused, for
+    // the next step's K0 (canon_row_sums' order: vector k of a band row on lane k of a 32-lane
+    // half-wave, W / V <= 32, the host checks); the same values and stores as the plain pass
+    const int nvr = W / V, nrows = r1 - r0, hw = tid >> 5, k = tid & 31;
+    double* rsb = a.rs + (size_t)b * C * H + r0;
+    for (int rb = 0; rb < nrows; rb += kThreads / 32) {   // uniform: every lane reaches the shuffles
+      const int rr = rb + hw;
+      const bool on = rr < nrows && k < nvr;
+      const int e = V * (rr * nvr + k), ii = r0 + rr, j = V * k;
+      const float* src = a.dx;
+      int rk[V];
+      size_t p0 = 0;
+      if (on) {
+        const uint32_t ci = colinfo[j];
+        const int te = (ii - h0) * txn + (int)(ci >> 16), tj = (int)(ci & 0xffffu);
+        const uint64_t m = tab_m[te];
+        const uint32_t bits = (uint32_t)(m >> tj) & ((1u << V) - 1u);
+        src = a.dx + (size_t)tab_t[te] * C * NCELL + tab_p[te] + (uint32_t)__popcll(m & ((1ull << tj) - 1ull));
+#pragma unroll
+        for (int kk = 0; kk < V; ++kk) rk[kk] = ((bits >> kk) & 1u) ? __popc(bits & ((1u << kk) - 1u)) : -1;
+        p0 = base + (size_t)e;
+      }
+      {   // alpha: x~_3 * post (computed above)
+        float f[V];
+        if (on) {
+          vf v;
+#pragma unroll
+          for (int kk = 0; kk < V; ++kk) v[kk] = f[kk] = at[(r0 - h0) * W + e + kk] * post[e + kk];
+          *reinterpret_cast<vf*>(ob + 3 * HW + p0) = v;
+        }
+        const double S = canon_butterfly32(on ? canon_vec_sum<V>(f) : 0.0);
+        if (k == 0 && rr < nrows) rsb[(size_t)3 * H + rr] = S;
+      }
+      for (int c0 = 0; c0 < C; c0 += CU) {
+        vf xq[CU], fq[CU];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+          const int c = c0 + u;
+          if (c >= C || c == 3 || !on) continue;
+          xq[u] = *reinterpret_cast<const vf*>(xb + (size_t)c * HW + p0);
+          fq[u] = *reinterpret_cast<const vfu*>(src + (size_t)c * NCELL);
+        }
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+          const int c = c0 + u;
+          if (c >= C || c == 3) continue;
+          float f[V];
+          if (on) {
+            const float sc = k2s[c], sh = k2s[32 + c];
+            vf v;
+#pragma unroll
+            for (int kk = 0; kk < V; ++kk) {
+              float d = 0.f;
+#pragma unroll
+              for (int r = 0; r <= kk; ++r) d = rk[kk] == r ? fq[u][r] : d;
+              v[kk] = f[kk] = k2_update(xq[u][kk], d, sc, sh, a.gain, g2);
+            }
+            *reinterpret_cast<vf*>(ob + (size_t)c * HW + p0) = v;
+          }
+          const double S = canon_butterfly32(on ? canon_vec_sum<V>(f) : 0.0);
+          if (k == 0 && rr < nrows) rsb[(size_t)c * H + rr] = S;
+        }
+      }
     }
   } else {
     // compact: one thread per cell vector, all channels; the vector's packed-field position and
@@ -1223,7 +1298,7 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
 #ifndef GNCA_K2_PRIO
 #define GNCA_K2_PRIO 3
 #endif
-template <int V, bool COMPACT, int CU = GNCA_K2_CU>
+template <int V, bool COMPACT, int CU = GNCA_K2_CU, bool ROWS = false>
 __global__ __launch_bounds__(kThreads) GNCA_K2_ATTR void gnca_k2_finalize(const K2Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float sh_norm[4 + 64 + 64];
@@ -1249,7 +1324,7 @@ __global__ __launch_bounds__(kThreads) GNCA_K2_ATTR void gnca_k2_finalize(const 
   // below K1 it was starved of issue slots and held its CU share longer (headline step 0.512 ->
   // 0.495 ms, profiles/r04_ab_k2_priority.txt)
   __builtin_amdgcn_s_setprio(GNCA_K2_PRIO);
-  k2_body<V, COMPACT, CU>(a, smem, sh_norm);
+  k2_body<V, COMPACT, CU, ROWS>(a, smem, sh_norm);
   GNCA_STAMP_END(a.stamps);
 }
 
@@ -1335,12 +1410,15 @@ struct K0Args {
   int8_t offs[2 * GNCA_MAX_OFFSETS];
 };
 
-// K0's first phase: the per-(channel, row) fp64 sums of x, one workgroup per (channel, sample) so that
-// a small batch still spreads over the chip (one workgroup per sample took 57 us for B=16 40^2)
+// K0's first phase: the per-(channel, row) fp64 sums of x in the canonical order (canon_row_sums), one
+// workgroup per (channel, sample) so that a small batch still spreads over the chip (one workgroup per
+// sample took 57 us for B=16 40^2); a rollout's later steps take them from the previous step's K2
+template <int V>
 __global__ __launch_bounds__(kThreads) void gnca_k0_rowsums(const float* x, double* rs, int C, int H, int W) {
-  const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const size_t HW = (size_t)H * W;
-  row_sums_f64<4>(x + ((size_t)b * C + c) * HW, 1, H, W, rs + ((size_t)b * C + c) * H, lane, wave, kThreads / 64);
+  canon_row_sums<V, 4>(x + ((size_t)b * C + c) * HW, H, W, rs + ((size_t)b * C + c) * H, tid >> 5, kThreads / 32,
+                       tid & 31);
 }
 
 __global__ __launch_bounds__(kThreads) void gnca_k0_offset_weights(const K0Args a) {
@@ -1413,6 +1491,68 @@ __global__ __launch_bounds__(kThreads) void gnca_k0_offset_weights(const K0Args 
       sum += logit[o];
     }
     for (int o = 0; o < K; ++o) a.offw[(size_t)b * K + o] = (float)(logit[o] / sum);
+  }
+}
+
+// gnca_k0_offset_weights for C = 16, d = 16, k <= 8 (the module's graph defaults): one wave per sample,
+// no LDS.  The LDS version (13.6 KB) never fits beside the other sub-batch stream's persistent K1
+// (~6.6 KB of a CU's LDS left), so in the zero-pad rollout it waited for that K1 to retire.  Lane l
+// holds channel / unit c = l & 15 and offsets p = l >> 4 and p + 4; every sum keeps the LDS
+// version's order (row sums in row order, dot products in channel / unit order): the same bits.
+__global__ __launch_bounds__(64) void gnca_k0_weights16(const K0Args a) {
+  const int b = blockIdx.x, l = threadIdx.x, c = l & 15, p = l >> 4;
+  const int H = a.H, W = a.W, K = a.k;
+  const double HW = (double)H * (double)W;
+  const double* rs = a.rs + ((size_t)b * 16 + c) * H;
+  auto rows = [&](int o, int* lo, int* hi) {   // the source rows the zero-padded shift keeps
+    const int dy = o < K ? a.offs[2 * o] : 0;
+    *lo = dy > 0 ? 0 : -dy;
+    *hi = dy > 0 ? H - dy : H;
+  };
+  int lo0, hi0, lo1, hi1;
+  rows(p, &lo0, &hi0);
+  rows(p + 4, &lo1, &hi1);
+  double tot = 0.0, s0 = 0.0, s1 = 0.0;
+#pragma unroll 8
+  for (int r = 0; r < H; ++r) {
+    const double v = rs[r];
+    tot += v;
+    if (r >= lo0 && r < hi0) s0 += v;
+    if (r >= lo1 && r < hi1) s1 += v;
+  }
+  const double xbar = tot / HW;
+  // qbar[e] (lane e of each 16-lane group): b_Q + W_Q xbar
+  double qb = (double)a.bq[c];
+  for (int cc = 0; cc < 16; ++cc) qb += (double)a.wq[c * 16 + cc] * __shfl(xbar, cc);
+  // pooled keys of this group's offsets (unit e = c): b_K * rows * W + W_K sco
+  double k0 = (double)a.bk[c] * (double)(hi0 > lo0 ? hi0 - lo0 : 0) * (double)W;
+  double k1 = (double)a.bk[c] * (double)(hi1 > lo1 ? hi1 - lo1 : 0) * (double)W;
+  for (int cc = 0; cc < 16; ++cc) {
+    const double wk = (double)a.wk[c * 16 + cc];
+    k0 += wk * __shfl(s0, 16 * p + cc);
+    k1 += wk * __shfl(s1, 16 * p + cc);
+  }
+  // logits of offsets p and p + 4: sum over units e in order (the same expression as the LDS version)
+  double L0 = 0.0, L1 = 0.0;
+  for (int e = 0; e < 16; ++e) {
+    const double q = __shfl(qb, 16 * p + e);
+    L0 += q * (__shfl(k0, 16 * p + e) / HW);
+    L1 += q * (__shfl(k1, 16 * p + e) / HW);
+  }
+  // softmax over the k offsets with the temperature |scaling| + 1e-6 (lane 0, in offset order)
+  double lg[8];
+#pragma unroll
+  for (int o = 0; o < 8; ++o) lg[o] = o < 4 ? __shfl(L0, 16 * o) : __shfl(L1, 16 * (o - 4));
+  if (l == 0) {
+    double mx = -INFINITY;
+    for (int o = 0; o < K; ++o) mx = fmax(mx, lg[o]);
+    const double T = fabs((double)a.scaling[0]) + 1e-6;
+    double sum = 0.0;
+    for (int o = 0; o < K; ++o) {
+      lg[o] = exp((lg[o] - mx) / T);
+      sum += lg[o];
+    }
+    for (int o = 0; o < K; ++o) a.offw[(size_t)b * K + o] = (float)(lg[o] / sum);
   }
 }
 
@@ -1846,8 +1986,12 @@ static void fill_k1(K1Args& k1, const gnca_step_desc* d, const gnca_weights* w, 
     k1.odl[o] = d->offsets[2 * o] * RW + (zp ? 0 : d->offsets[2 * o + 1]);
 }
 
+#ifndef GNCA_K0_LDS
+#define GNCA_K0_LDS 0   // A/B builds: 1 = the LDS offset-weights kernel for every shape
+#endif
+// rows_ready: the row sums of x are already in the workspace (the previous step's K2 wrote them)
 static int launch_k0(const gnca_step_desc* d, const gnca_weights* w, const Plan& P, const float* x,
-                     char* ws, hipStream_t st) {
+                     char* ws, hipStream_t st, bool rows_ready = false) {
   K0Args k0;
   memset(&k0, 0, sizeof(k0));
   k0.x = x; k0.wq = w->wq; k0.bq = w->bq; k0.wk = w->wk; k0.bk = w->bk; k0.scaling = w->scaling;
@@ -1856,13 +2000,18 @@ static int launch_k0(const gnca_step_desc* d, const gnca_weights* w, const Plan&
   k0.rs = rs;
   k0.B = d->B; k0.C = d->C; k0.H = d->H; k0.W = d->W; k0.d = d->d_model; k0.k = P.k;
   if (d->B > 65535) return GNCA_ERR_UNSUPPORTED;   // (grid y)
-  hipLaunchKernelGGL(gnca_k0_rowsums, dim3(d->C, d->B), dim3(kThreads), 0, st, x, rs, d->C, d->H, d->W);
+  if (!rows_ready)
+    hipLaunchKernelGGL((d->W & 3) == 0 ? gnca_k0_rowsums<4> : gnca_k0_rowsums<1>, dim3(d->C, d->B), dim3(kThreads),
+                       0, st, x, rs, d->C, d->H, d->W);
   for (int o = 0; o < 2 * P.k; ++o) k0.offs[o] = d->offsets[o];
   const size_t lds = ((size_t)d->C * d->H + d->C + d->d_model + P.k + (size_t)d->C * P.k +
                       (size_t)P.k * d->d_model) * sizeof(double) + 2 * (size_t)d->d_model * d->C * sizeof(float);
   if (lds > 64 * 1024) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gnca_k0_offset_weights),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(gnca_k0_offset_weights, dim3(d->B), dim3(kThreads), lds, st, k0);
+  if (d->C == 16 && d->d_model == 16 && P.k <= 8 && !GNCA_K0_LDS)
+    hipLaunchKernelGGL(gnca_k0_weights16, dim3(d->B), dim3(64), 0, st, k0);
+  else
+    hipLaunchKernelGGL(gnca_k0_offset_weights, dim3(d->B), dim3(kThreads), lds, st, k0);
   return check_launch();
 }
 
@@ -1936,7 +2085,14 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   if (set != 0 && !P.fold_any) return GNCA_ERR_INVALID;
   const FieldSet fs = field_set(P, wsb, set);
   int rc;
-  if ((phases & GNCA_PHASE_K0) && P.need_k0 && (rc = launch_k0(d, w, P, x, wsb, st)) != GNCA_OK)
+  // compact update field (rollout mode): K1 packs the live cells' dx per tile, K2 unpacks them
+  compact = compact && P.compact_ok && !active && !want_attn;
+  // zero-padded shift in a rollout on the compact field: K2 also writes the new state's row sums, so
+  // the next step's K0 skips its pass over the state (the alive-byte hand-over's condition, plus
+  // rows of at most 32 cell vectors: K2's fused sums use one 32-lane half-wave per row)
+  const bool rows_k2 = P.need_k0 && compact && d->W / ((d->W & 3) == 0 ? 4 : 1) <= 32;
+  if ((phases & GNCA_PHASE_K0) && P.need_k0 &&
+      (rc = launch_k0(d, w, P, x, wsb, st, rows_k2 && alive_in)) != GNCA_OK)
     return rc;
   // attention with no offsets (k == 0, or radius 1): the reference returns zeros unnormalised
   if (want_attn && !P.graph_on) {
@@ -1961,8 +2117,6 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
                        d->H, d->W, d->alpha_thr, d->graph_alpha_thr);
     if ((rc = check_launch()) != GNCA_OK) return rc;
   }
-  // compact update field (rollout mode): K1 packs the live cells' dx per tile, K2 unpacks them
-  compact = compact && P.compact_ok && !active && !want_attn;
   uint64_t* rmask = fs.rmask;
   uint32_t* rpre = fs.rpre;
   float* dxa = fs.dxa;
@@ -1993,6 +2147,7 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   k2.gain = d->update_gain; k2.thr = d->alpha_thr; k2.eps = d->gn_eps;
   k2.gthr = d->graph_alpha_thr;
   k2.alive_out = alive_out ? alive : nullptr;
+  k2.rs = (rows_k2 && alive_out) ? reinterpret_cast<double*>(wsb + P.off_rs) : nullptr;
   k2.active = active;
   // GNCA_K2_ZIGZAG=0 (measurement builds only) keeps the plain sample order; measured B=1024: 0.690
   // -> 0.679 ms/step (K2 0.182 -> 0.180 ms, the next K1 -0.5 %)
@@ -2011,7 +2166,9 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
     if ((compact ? P.total2_c : P.total2) > stamp_cap) return GNCA_ERR_INVALID;
     k2.stamps = stamps + 2 * (size_t)stamp_cap;
   }
-  auto k2fn = compact ? (k2_co ? ((d->W & 3) == 0 ? gnca_k2_finalize<4, true> : gnca_k2_finalize<1, true>)
+  auto k2fn = compact ? (k2.rs ? ((d->W & 3) == 0 ? gnca_k2_finalize<4, true, GNCA_K2_CU_ROWS, true>
+                                                   : gnca_k2_finalize<1, true, GNCA_K2_CU_ROWS, true>)
+                        : k2_co ? ((d->W & 3) == 0 ? gnca_k2_finalize<4, true> : gnca_k2_finalize<1, true>)
                               : ((d->W & 3) == 0 ? gnca_k2_finalize<4, true, GNCA_K2_CU_ALONE>
                                                  : gnca_k2_finalize<1, true, GNCA_K2_CU_ALONE>))
                       : ((d->W & 3) == 0 ? gnca_k2_finalize<4, false> : gnca_k2_finalize<1, false>);

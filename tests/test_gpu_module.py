@@ -448,15 +448,17 @@ def test_masked_step_many_tiles_per_workgroup(dev):
     assert torch.equal(masked[~act], x[~act])
 
 
-def test_subbatch_rollout_and_pieces_bitwise(dev):
+@pytest.mark.parametrize("zp", [False, True])
+def test_subbatch_rollout_and_pieces_bitwise(dev, zp):
     """A large-batch rollout of a K1 without a fold variant (the 40^2 trainer canvas's 8x20 tiles)
     runs as 2 sub-batches on two streams (one sub-batch's K2 beside the other's K1): bitwise the
     states of repeated single steps; and a rollout issued in pieces with the alive masks handed over
     through the workspace (gnca_rollout_ex_f32 ALIVE_OUT / ALIVE_IN) is bitwise the one-call
-    rollout."""
+    rollout.  Zero-padded shift: the rollout's K2 also hands the next step's K0 the new state's row
+    sums (canon_row_sums' order), which single steps compute in K0's own pass: the same bits."""
     from graph_neural_cellular_automata_amd import _lib as L
     from graph_neural_cellular_automata_amd import step as S
-    m = _trained_like(dev, seed=9)
+    m = _trained_like(dev, zp=zp, seed=9)
     B, steps, H = 384, 5, 40
     x = _state(B, 16, H, H, dev, seed=29)
     random.seed(19)
@@ -468,7 +470,8 @@ def test_subbatch_rollout_and_pieces_bitwise(dev):
 
     def desc(t):
         return S.make_desc(B=B, C=16, H=H, W=H, hidden=128, d_model=16, offsets=offs[t],
-                           flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE,
+                           flags=L.GRAPH | L.USE_GROUPNORM | L.HIDDEN_ONLY | L.ALIVE_TO_ALIVE |
+                           (L.ZERO_PAD_SHIFT if zp else 0),
                            update_gain=0.05, alpha_thr=0.12, message_gain=0.25, fire_rate=0.5,
                            fire_mode=L.FIRE_HASH, rng_seed=3, rng_step=t, sample_base=7)
 
