@@ -1512,23 +1512,40 @@ __global__ __launch_bounds__(64) void gnca_k0_weights16(const K0Args a) {
   int lo0, hi0, lo1, hi1;
   rows(p, &lo0, &hi0);
   rows(p + 4, &lo1, &hi1);
+  // every load first (the projection rows of this lane's unit, then the row sums 24 at a time):
+  // the kernel is a latency chain between a sub-batch's K2 and its K1 in the zero-pad rollout
+  float wqv[16], wkv[16];
+#pragma unroll
+  for (int cc = 0; cc < 16; ++cc) {
+    wqv[cc] = a.wq[c * 16 + cc];
+    wkv[cc] = a.wk[c * 16 + cc];
+  }
+  const float bqv = a.bq[c], bkv = a.bk[c];
   double tot = 0.0, s0 = 0.0, s1 = 0.0;
-#pragma unroll 8
-  for (int r = 0; r < H; ++r) {
-    const double v = rs[r];
-    tot += v;
-    if (r >= lo0 && r < hi0) s0 += v;
-    if (r >= lo1 && r < hi1) s1 += v;
+  constexpr int RB = 24;
+  for (int rb = 0; rb < H; rb += RB) {
+    double v[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) v[i] = rb + i < H ? rs[rb + i] : 0.0;
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int r = rb + i;
+      if (r < H) {
+        tot += v[i];
+        if (r >= lo0 && r < hi0) s0 += v[i];
+        if (r >= lo1 && r < hi1) s1 += v[i];
+      }
+    }
   }
   const double xbar = tot / HW;
   // qbar[e] (lane e of each 16-lane group): b_Q + W_Q xbar
-  double qb = (double)a.bq[c];
-  for (int cc = 0; cc < 16; ++cc) qb += (double)a.wq[c * 16 + cc] * __shfl(xbar, cc);
+  double qb = (double)bqv;
+  for (int cc = 0; cc < 16; ++cc) qb += (double)wqv[cc] * __shfl(xbar, cc);
   // pooled keys of this group's offsets (unit e = c): b_K * rows * W + W_K sco
-  double k0 = (double)a.bk[c] * (double)(hi0 > lo0 ? hi0 - lo0 : 0) * (double)W;
-  double k1 = (double)a.bk[c] * (double)(hi1 > lo1 ? hi1 - lo1 : 0) * (double)W;
+  double k0 = (double)bkv * (double)(hi0 > lo0 ? hi0 - lo0 : 0) * (double)W;
+  double k1 = (double)bkv * (double)(hi1 > lo1 ? hi1 - lo1 : 0) * (double)W;
   for (int cc = 0; cc < 16; ++cc) {
-    const double wk = (double)a.wk[c * 16 + cc];
+    const double wk = (double)wkv[cc];
     k0 += wk * __shfl(s0, 16 * p + cc);
     k1 += wk * __shfl(s1, 16 * p + cc);
   }
