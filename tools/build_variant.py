@@ -11,6 +11,7 @@ sys.path.insert(0, ROOT)
 import __graft_entry__ as G  # noqa: E402
 
 out, flags = sys.argv[1], sys.argv[2:]
+os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
 objdir = os.path.join(ROOT, "build", "obj_" + os.path.basename(out).replace(".so", ""))
 os.makedirs(objdir, exist_ok=True)
 procs, objs = [], []
