@@ -201,6 +201,7 @@ int gnca_rollout_f32(const gnca_step_desc* desc, const gnca_weights* w, int32_t 
  * piece's offsets while the device runs the previous piece) computes exactly the one-call result
  * when the pieces hand the alive masks over through the shared workspace:
  *   GNCA_ROLLOUT_ALIVE_OUT  the last step's K2 also writes the next state's alive masks into `ws`
+ *                           (zero-padded shift on the compact field: and its fp64 row sums for K0)
  *   GNCA_ROLLOUT_ALIVE_IN   the first step's K1 reads them from `ws` (written by the previous call
  *                           with ALIVE_OUT on the same workspace; x = that call's x_final)
  * Both need 0 <= alpha_thr <= graph_alpha_thr (else GNCA_ERR_INVALID).  flags = 0 is gnca_rollout_f32.
