@@ -1,0 +1,135 @@
+"""GPU parity over seeded random configurations of the module (beyond the golden fixtures' grid):
+random batch, canvas (ragged, tiny, non-multiple-of-4), channel count, hidden width, graph radius
+and offset count, torus / zero-padded shift, GroupNorm on / off, hidden_only, alive_to_alive,
+fire rate and message gain.  Each case runs one module step with the reference's draws
+(``random.sample`` of the offsets, ``torch.rand`` for the fire mask) and compares it with the f64
+oracle (oracle/nca_oracle.py) at the parity tolerance of tests/test_gpu_parity.py; the graph
+cases also run a 3-step rollout through the C ABI, bitwise against 3 single steps.
+
+The seeds are fixed and the kernels and the oracle deterministic, so the set is the same on
+every run.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nca_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ATOL, RTOL = 2e-6, 1e-5
+N_CASES = 32
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    return torch.device("cuda:0")
+
+
+def _config(seed):
+    g = np.random.default_rng(1000 + seed)
+    graph = bool(g.random() < 0.75)
+    C = int(g.choice([4, 8, 12, 16, 16, 16, 20, 32]))
+    hidden = int(g.choice([32, 64, 128, 128]))
+    B = int(g.integers(1, 4))
+    H = int(g.integers(5, 81))
+    W = int(g.integers(5, 81))
+    while B * H * W > 12000:
+        H, W = max(5, H * 3 // 4), max(5, W * 3 // 4)
+    return dict(graph=graph, C=C, hidden=hidden, B=B, H=H, W=W,
+                radius=int(g.integers(1, 6)), K=int(g.choice([0, 4, 8, 8, 16])),
+                zp=bool(g.random() < 0.5), gn=bool(g.random() < 0.8),
+                hidden_only=bool(g.random() < 0.7), a2a=bool(g.random() < 0.7),
+                fire_rate=float(g.choice([1.0, 0.5, 0.75])), msg=float(g.choice([0.0, 0.25, 0.5])),
+                d_model=int(g.choice([8, 16])), gain=float(g.choice([0.05, 0.1])),
+                thr=float(g.choice([0.1, 0.12])))
+
+
+def _model(cfg, dev, seed):
+    from graph_neural_cellular_automata_amd import NeuralCA, NeuralCAGraph
+    torch.manual_seed(seed)
+    if cfg["graph"]:
+        m = NeuralCAGraph(cfg["C"], cfg["hidden"], update_gain=cfg["gain"], alpha_thr=cfg["thr"],
+                          use_groupnorm=cfg["gn"], message_gain=cfg["msg"], hidden_only=cfg["hidden_only"],
+                          graph_d_model=cfg["d_model"], graph_attention_radius=cfg["radius"],
+                          graph_num_neighbors=cfg["K"], graph_alive_to_alive=cfg["a2a"],
+                          graph_zero_padded_shift=cfg["zp"])
+    else:
+        m = NeuralCA(cfg["C"], cfg["hidden"], update_gain=cfg["gain"], alpha_thr=cfg["thr"],
+                     use_groupnorm=cfg["gn"])
+    m = m.to(dev).eval()
+    with torch.no_grad():
+        m.update_net[2].weight.normal_(0, 0.05)
+        if cfg["gn"]:
+            m.norm.weight.uniform_(0.5, 1.5)
+            m.norm.bias.uniform_(-0.2, 0.2)
+    return m
+
+
+def _state(cfg, dev, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.rand(cfg["B"], cfg["C"], cfg["H"], cfg["W"], device=dev, generator=g)
+    x[:, 4:] = torch.randn(cfg["B"], cfg["C"] - 4, cfg["H"], cfg["W"], device=dev, generator=g)
+    return x
+
+
+def _oracle_cfg(cfg):
+    return dict(update_gain=cfg["gain"], alpha_thr=cfg["thr"], use_groupnorm=cfg["gn"], graph=cfg["graph"],
+                message_gain=cfg["msg"], hidden_only=cfg["hidden_only"], zero_padded_shift=cfg["zp"],
+                alive_to_alive=cfg["a2a"])
+
+
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_random_config_step_matches_oracle(dev, seed):
+    cfg = _config(seed)
+    m = _model(cfg, dev, seed)
+    x = _state(cfg, dev, seed)
+    # the reference's draws: random.sample of the offsets (graph), then torch.rand for the fire mask
+    random.seed(seed)
+    chosen = m.graph.sample_offsets() if cfg["graph"] else None
+    st = torch.cuda.get_rng_state(dev)
+    fire = None
+    if cfg["fire_rate"] < 1.0:
+        fire = (torch.rand(cfg["B"], 1, cfg["H"], cfg["W"], device=dev) <= cfg["fire_rate"]).float()
+    torch.cuda.set_rng_state(st, dev)
+    random.seed(seed)
+    with torch.no_grad():
+        out = m(x, fire_rate=cfg["fire_rate"])
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    ref = O.nca_step(x.cpu().numpy().astype(np.float64), p, _oracle_cfg(cfg), chosen=chosen,
+                     fire_mask=None if fire is None else fire.cpu().numpy().astype(np.float64))
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL, atol=ATOL, err_msg=str(cfg))
+
+
+@pytest.mark.parametrize("seed", [s for s in range(N_CASES) if _config(s)["graph"]])
+def test_random_config_rollout_equals_steps(dev, seed):
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    cfg = _config(seed)
+    m = _model(cfg, dev, seed)
+    x = _state(cfg, dev, seed).contiguous()
+    random.seed(seed)
+    offs = [m.graph.sample_offsets() for _ in range(3)]
+    tensors = dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight, b1=m.update_net[0].bias,
+                   w2=m.update_net[2].weight, **m.graph.weight_tensors())
+    if cfg["gn"]:
+        tensors.update(gn_weight=m.norm.weight, gn_bias=m.norm.bias)
+    w, keep = S.make_weights(tensors)
+    flags = m.graph.flags(False) | (L.USE_GROUPNORM if cfg["gn"] else 0) | (L.HIDDEN_ONLY if cfg["hidden_only"] else 0)
+
+    def desc(t):
+        return S.make_desc(B=cfg["B"], C=cfg["C"], H=cfg["H"], W=cfg["W"], hidden=cfg["hidden"],
+                           d_model=cfg["d_model"], offsets=offs[t], flags=flags, update_gain=cfg["gain"],
+                           alpha_thr=cfg["thr"], message_gain=cfg["msg"], fire_rate=cfg["fire_rate"],
+                           fire_mode=L.FIRE_HASH if cfg["fire_rate"] < 1.0 else L.FIRE_NONE,
+                           rng_seed=seed, rng_step=t)
+
+    r = S.rollout(desc(0), w, x, 3, offs)
+    cur = x
+    for t in range(3):
+        cur, _ = S.step(desc(t), w, cur)
+    assert torch.equal(r, cur), str(cfg)
