@@ -3,8 +3,9 @@ random batch, canvas (ragged, tiny, non-multiple-of-4), channel count, hidden wi
 and offset count, torus / zero-padded shift, GroupNorm on / off, hidden_only, alive_to_alive,
 fire rate and message gain.  Each case runs one module step with the reference's draws
 (``random.sample`` of the offsets, ``torch.rand`` for the fire mask) and compares it with the f64
-oracle (oracle/nca_oracle.py) at the parity tolerance of tests/test_gpu_parity.py; the graph
-cases also run a 3-step rollout through the C ABI, bitwise against 3 single steps.
+oracle (oracle/nca_oracle.py) at the parity tolerance of tests/test_gpu_parity.py and its
+backward against the f64 VJP oracle at tests/test_gpu_grad.py's; the graph cases also run a 3-step
+rollout through the C ABI, bitwise against 3 single steps.
 
 The seeds are fixed and the kernels and the oracle deterministic, so the set is the same on
 every run.
@@ -133,3 +134,47 @@ def test_random_config_rollout_equals_steps(dev, seed):
     for t in range(3):
         cur, _ = S.step(desc(t), w, cur)
     assert torch.equal(r, cur), str(cfg)
+
+
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_random_config_backward_matches_oracle(dev, seed):
+    """The module's backward (gnca_step_bwd_f32 through autograd) on the same random configurations
+    against the f64 VJP oracle (oracle/nca_oracle_vjp.py), per gradient tensor within
+    2e-5 * max|ref| + 1e-6 (tests/test_gpu_grad.py).  A parameter the module leaves without a
+    gradient (no offsets drawn, the frozen perception, gate_mlp) must have an all-zero reference."""
+    from oracle import nca_oracle_vjp as V
+    cfg = _config(seed)
+    m = _model(cfg, dev, seed)
+    if cfg["graph"]:
+        with torch.no_grad():   # pooled-logit gradients of a visible size in zero-pad mode
+            m.graph.query_proj.weight.normal_(0, 0.3)
+            m.graph.key_proj.weight.normal_(0, 0.3)
+    x = _state(cfg, dev, seed).requires_grad_(True)
+    gy = torch.randn(x.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(77 + seed))
+    random.seed(seed)
+    chosen = m.graph.sample_offsets() if cfg["graph"] else None
+    st = torch.cuda.get_rng_state(dev)
+    fire = None
+    if cfg["fire_rate"] < 1.0:
+        fire = (torch.rand(cfg["B"], 1, cfg["H"], cfg["W"], device=dev) <= cfg["fire_rate"]).double().cpu().numpy()
+    torch.cuda.set_rng_state(st, dev)
+    random.seed(seed)
+    out = m(x, fire_rate=cfg["fire_rate"])
+    (out * gy).sum().backward()
+    torch.cuda.synchronize()
+    p = {k: v.detach().double().cpu().numpy() for k, v in m.state_dict().items()}
+    gx, grads = V.nca_step_vjp(x.detach().double().cpu().numpy(), p, _oracle_cfg(cfg),
+                               gy.double().cpu().numpy(), chosen=chosen, fire_mask=fire)
+    ref = dict(grads, gx=gx)
+    got = {n: q.grad for n, q in m.named_parameters() if q.grad is not None}
+    got["gx"] = x.grad
+    for k, r in ref.items():
+        scale = float(np.abs(r).max())
+        if k not in got:
+            assert scale == 0.0, (k, scale, cfg)
+            continue
+        g = got[k].detach().cpu().numpy().reshape(r.shape).astype(np.float64)
+        err = float(np.abs(g - r).max())
+        assert np.isfinite(g).all(), (k, cfg)
+        assert err <= 2e-5 * scale + 1e-6, (k, f"err={err:.3e} scale={scale:.3e}", cfg)
+    assert set(got) <= set(ref), (sorted(set(got) - set(ref)), cfg)
