@@ -178,3 +178,39 @@ def test_random_config_backward_matches_oracle(dev, seed):
         assert np.isfinite(g).all(), (k, cfg)
         assert err <= 2e-5 * scale + 1e-6, (k, f"err={err:.3e} scale={scale:.3e}", cfg)
     assert set(got) <= set(ref), (sorted(set(got) - set(ref)), cfg)
+
+
+def _config_split(seed):
+    """The 16-channel, hidden-128 shapes the split (bf16x6) K1 variants serve: canvases of whole
+    tiles, graph or classic, radius <= 4, torus or zero-padded shift."""
+    g = np.random.default_rng(5000 + seed)
+    H, W = [(40, 40), (72, 72), (48, 72), (24, 36), (80, 40), (96, 96), (72, 48), (64, 64)][int(g.integers(0, 8))]
+    graph = bool(g.random() < 0.75)
+    return dict(graph=graph, C=16, hidden=128, B=int(g.choice([1, 2, 5, 12])), H=H, W=W,
+                radius=int(g.integers(1, 5)), K=int(g.choice([4, 8, 8])), zp=bool(g.random() < 0.4),
+                gn=bool(g.random() < 0.85), hidden_only=bool(g.random() < 0.8), a2a=bool(g.random() < 0.8),
+                fire_rate=float(g.choice([1.0, 0.5])), msg=float(g.choice([0.25, 0.5])),
+                d_model=16, gain=float(g.choice([0.05, 0.1])), thr=float(g.choice([0.1, 0.12])))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_split_k1_shapes_match_oracle(dev, seed):
+    """One module step on the split K1's shapes (random batch, canvas, graph radius, modes) against
+    the f64 oracle at the parity tolerance."""
+    cfg = _config_split(seed)
+    m = _model(cfg, dev, seed)
+    x = _state(cfg, dev, seed)
+    random.seed(seed)
+    chosen = m.graph.sample_offsets() if cfg["graph"] else None
+    st = torch.cuda.get_rng_state(dev)
+    fire = None
+    if cfg["fire_rate"] < 1.0:
+        fire = (torch.rand(cfg["B"], 1, cfg["H"], cfg["W"], device=dev) <= cfg["fire_rate"]).float()
+    torch.cuda.set_rng_state(st, dev)
+    random.seed(seed)
+    with torch.no_grad():
+        out = m(x, fire_rate=cfg["fire_rate"])
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    ref = O.nca_step(x.cpu().numpy().astype(np.float64), p, _oracle_cfg(cfg), chosen=chosen,
+                     fire_mask=None if fire is None else fire.cpu().numpy().astype(np.float64))
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL, atol=ATOL, err_msg=str(cfg))
