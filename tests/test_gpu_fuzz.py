@@ -214,3 +214,49 @@ def test_split_k1_shapes_match_oracle(dev, seed):
     ref = O.nca_step(x.cpu().numpy().astype(np.float64), p, _oracle_cfg(cfg), chosen=chosen,
                      fire_mask=None if fire is None else fire.cpu().numpy().astype(np.float64))
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL, atol=ATOL, err_msg=str(cfg))
+
+
+@pytest.mark.parametrize("seed", [s for s in range(N_CASES) if _config(s)["graph"]])
+def test_random_config_attention_matches_oracle(dev, seed):
+    """return_attention=True on the random graph configurations: the state and the normalised
+    attention map against the f64 oracle (map within 2e-5, tests/test_gpu_parity.py)."""
+    cfg = _config(seed)
+    m = _model(cfg, dev, seed)
+    x = _state(cfg, dev, seed)
+    random.seed(seed)
+    chosen = m.graph.sample_offsets()
+    st = torch.cuda.get_rng_state(dev)
+    fire = None
+    if cfg["fire_rate"] < 1.0:
+        fire = (torch.rand(cfg["B"], 1, cfg["H"], cfg["W"], device=dev) <= cfg["fire_rate"]).float()
+    torch.cuda.set_rng_state(st, dev)
+    random.seed(seed)
+    with torch.no_grad():
+        out, attn = m(x, fire_rate=cfg["fire_rate"], return_attention=True)
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    ref, ref_attn = O.nca_step(x.cpu().numpy().astype(np.float64), p, _oracle_cfg(cfg), chosen=chosen,
+                               fire_mask=None if fire is None else fire.cpu().numpy().astype(np.float64),
+                               return_attention=True)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL, atol=ATOL, err_msg=str(cfg))
+    np.testing.assert_allclose(attn.cpu().numpy(), ref_attn, rtol=0, atol=2e-5, err_msg=str(cfg))
+
+
+@pytest.mark.parametrize("seed", range(0, N_CASES, 2))
+def test_random_config_masked_step_equals_subbatch(dev, seed):
+    """The active-sample mask (the trainers' x[m] = model(x[m])) on the random configurations: the
+    masked module step equals the step of the active sub-batch bitwise, inactive samples pass through
+    (uniform fire draws on the whole batch, as the module's mask contract says)."""
+    cfg = dict(_config(seed), B=4)
+    m = _model(cfg, dev, seed)
+    x = _state(cfg, dev, seed)
+    active = torch.tensor([True, False, True, True], device=dev)
+    random.seed(seed)
+    st = torch.cuda.get_rng_state(dev)
+    with torch.no_grad():
+        out = m(x, fire_rate=1.0, active=active)
+    torch.cuda.set_rng_state(st, dev)
+    random.seed(seed)
+    with torch.no_grad():
+        sub = m(x[active].contiguous(), fire_rate=1.0)
+    assert torch.equal(out[active], sub), str(cfg)
+    assert torch.equal(out[~active], x[~active])
