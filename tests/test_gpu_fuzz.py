@@ -260,3 +260,43 @@ def test_random_config_masked_step_equals_subbatch(dev, seed):
         sub = m(x[active].contiguous(), fire_rate=1.0)
     assert torch.equal(out[active], sub), str(cfg)
     assert torch.equal(out[~active], x[~active])
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_split_k1_rollout_plans_equal_steps(dev, seed):
+    """Rollouts of the split K1's shapes at batches that take every rollout plan (the dense fold of
+    small batches, the compact field on one stream, the two-stream sub-batch pipeline), 4 steps,
+    bitwise against 4 single steps; the plan is recorded in the assertion message."""
+    from graph_neural_cellular_automata_amd import _lib as L
+    from graph_neural_cellular_automata_amd import step as S
+    cfg = _config_split(seed)
+    cfg["B"] = [4, 8, 64, 160, 384][seed % 5]
+    cfg["graph"] = seed % 3 != 2
+    m = _model(cfg, dev, seed)
+    x = _state(cfg, dev, seed).contiguous()
+    random.seed(seed)
+    offs = [m.graph.sample_offsets() if cfg["graph"] else [] for _ in range(4)]
+    tensors = dict(perception=m.perception.conv.weight, w1=m.update_net[0].weight, b1=m.update_net[0].bias,
+                   w2=m.update_net[2].weight)
+    if cfg["graph"]:
+        tensors.update(m.graph.weight_tensors())
+    if cfg["gn"]:
+        tensors.update(gn_weight=m.norm.weight, gn_bias=m.norm.bias)
+    w, keep = S.make_weights(tensors)
+    flags = ((m.graph.flags(False) | (L.HIDDEN_ONLY if cfg["hidden_only"] else 0)) if cfg["graph"] else 0) | \
+        (L.USE_GROUPNORM if cfg["gn"] else 0)
+
+    def desc(t):
+        return S.make_desc(B=cfg["B"], C=16, H=cfg["H"], W=cfg["W"], hidden=128, d_model=16,
+                           offsets=offs[t], flags=flags, update_gain=cfg["gain"], alpha_thr=cfg["thr"],
+                           message_gain=cfg["msg"] if cfg["graph"] else 0.0, fire_rate=cfg["fire_rate"],
+                           fire_mode=L.FIRE_HASH if cfg["fire_rate"] < 1.0 else L.FIRE_NONE,
+                           rng_seed=seed, rng_step=t)
+
+    plan = (S.k1_variant(desc(0))[0], "subs", S.rollout_subs(desc(0)), "fold", S.rollout_fold(desc(0)),
+            "compact", S.rollout_compact(desc(0)))
+    r = S.rollout(desc(0), w, x, 4, offs)
+    cur = x
+    for t in range(4):
+        cur, _ = S.step(desc(t), w, cur)
+    assert torch.equal(r, cur), (plan, cfg)
