@@ -707,6 +707,7 @@ def main():
         raise SystemExit("bench: the stamped rollout differs from the timed rollout")
     sv = stamps.view(args.steps, nsub, 2, cap, 2).cpu().numpy()
     dur = np.zeros((args.steps, nsub, 2))
+    tails = []                          # per K1 launch: (last workgroup end - median end) / span
     ivs = ([], [])                      # every K1 / K2 launch's [start, end] in ticks
     first, last = None, None
     for t in range(args.steps):
@@ -719,6 +720,8 @@ def main():
                     raise SystemExit(f"bench: no stamps from step {t} sub-batch {j} kernel {k}")
                 t0_, t1_ = int(sv[t, j, k, used, 0].min()), int(sv[t, j, k, used, 1].max())
                 dur[t, j, k] = (t1_ - t0_) * 1e-5          # 100 MHz ticks -> ms
+                if k == 0 and t1_ > t0_:   # the launch's tail: last workgroup end - median end, of its span
+                    tails.append((t1_ - float(np.median(sv[t, j, k, used, 1]))) / (t1_ - t0_))
                 ivs[k].append((t0_, t1_))
                 first = t0_ if first is None else min(first, t0_)
                 last = t1_ if last is None else max(last, t1_)
@@ -884,6 +887,7 @@ def main():
             "rank_state_checksums": rank_sums,
             "k1_k2_ms_vs_step": (k1_ms + k2_ms) / ms,   # > 1 only where sub-batches overlap K2 with K1
             "device_timeline": {"stamped_rollout_ms_per_step": stamped_ms,
+                                "k1_tail_frac": float(np.mean(tails)) if tails else None,
                                 "first_k1_start_to_last_k2_end_ms_per_step": span_ms,
                                 "sub_batches": nsub,
                                 "k1_ms": k1_ms, "k2_ms": k2_ms,
