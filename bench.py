@@ -10,7 +10,8 @@ counter RNG keyed by global sample index, so the N-GPU run computes exactly the 
 1-GPU run would for the same samples.  ``--config c2|c3|c5`` runs the other BASELINE.json GPU
 configs (classic B=8; graph B=8; 32ch 128^2 r=5 K=16) with the same harness.
 
-Multi-GPU: one process per GPU, B samples per rank (weak scaling), no collective on the data path;
+Multi-GPU: one process per GPU, B samples per rank (weak scaling; ``--scaling strong``: a fixed global
+batch B split B/N per rank, C4's fixed pool), no collective on the data path;
 barrier + synchronize around the timed region, max time over ranks.  Launched either by
 ``torch.distributed.run --nproc-per-node N bench.py --gpus N`` or as plain ``bench.py --gpus N``,
 which starts the N ranks itself (torch.distributed.run on 127.0.0.1) before touching the GPU.
@@ -125,7 +126,12 @@ def parse():
                          "(20 timed steps after 5 warmup steps: 8.47 G/s without, 9.57 G/s with)")
     ap.add_argument("--config", default="headline", choices=sorted(WORKLOADS),
                     help="rollout workload (BASELINE.json configs); default: the roofline headline")
-    ap.add_argument("--batch", type=int, default=None, help="samples per GPU (default: the config's)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="samples per GPU (weak scaling) or in the whole job (strong); default: the config's")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak (default): --batch samples per GPU, the job grows with N.  strong: a fixed "
+                         "global batch (--batch, default the config's: C4's pool of 1024) split B/N per "
+                         "rank, as a fixed sample pool sharded over N GPUs")
     ap.add_argument("--size", type=int, default=None, help="canvas (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=24.0,
                     help="wall budget of the CPU baseline (rank 0, N=1 only), split over its entries")
@@ -577,6 +583,10 @@ def main():
     wl = WORKLOADS[args.config]
     C, R, K, graph = wl["C"], wl["R"], wl["K"], wl["graph"]
     B = args.batch or wl["B"]
+    if args.scaling == "strong":   # a fixed global batch: this rank's share (global samples rank*B ..)
+        if B % world:
+            raise SystemExit(f"bench: --scaling strong needs the global batch {B} divisible by {world} ranks")
+        B //= world
     H = args.size or wl["H"]
     offsets_table = build_offsets(R) if graph else []
     w, w_keep = weight_struct(load_weights(dev, wl), wl)   # w_keep owns the tensors w points at
@@ -877,7 +887,7 @@ def main():
             "value": value, "unit": "cell-updates/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "gpu_warmup": {"ms": args.gpu_warmup_ms, "steps": gw_steps},
             "ms_per_step": ms,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic state (RGB,alpha~U(0,1), hidden~N(0,1)); {wdesc} weights from the "
                     f"committed golden fixture",
             "config": {"workload": wl["name"], "config": args.config,

@@ -129,9 +129,8 @@ def load_checkpoint(payload, model, optimizer=None, scheduler=None, pool=None) -
                       f"stream", flush=True)
             else:
                 pool.set_rng_state(ranks[pool.rank])
-        elif pool.rank == 0:   # a single unlabelled stream (older checkpoints): the saving rank's,
-            pool.set_rng_state(saved)   # which was rank 0 (the trainers save from rank 0 only)
-        else:
-            print(f"[warn] checkpoint holds one unlabelled pool stream (rank 0's): rank {pool.rank} "
-                  f"keeps its fresh stream", flush=True)
+        else:   # a single unlabelled stream (older checkpoints): its world size is not recorded, so
+                # the sharding it was drawn for may differ (a one-rank pool has no private stream)
+            print(f"[warn] checkpoint holds one unlabelled pool stream of an unknown world size: rank "
+                  f"{pool.rank} of {pool.world} keeps its fresh stream", flush=True)
     return int(payload.get("epoch", 0)) + 1

@@ -1058,11 +1058,6 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   BPROF_STORE;
 }
 
-// BB on the split bf16 arithmetic for C = 16, hidden = 128 (A/B builds only: slower, see bwd_plan)
-#ifdef GNCA_BB_SPLIT
-#include "gnca_bb_split.h"
-#endif
-
 // ------------------------------------------------------------------------------------------
 // BC: adjoint of the perception (zero-padded 3x3 correlation) and of the gather
 // ------------------------------------------------------------------------------------------
@@ -1248,7 +1243,8 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   // the reference's frozen identity / Sobel bank (the module's perception, always, in practice)?
   // Then the adjoint reads only the 13 taps with nonzero weights, with the weights as constants:
   // the same nonzero products in the same order as the generic loop (a zero-weight tap adds +0 to
-  // a sum that is never -0), so bitwise the same gx
+  // a sum that is never -0), so bitwise the same gx for finite dY (with an Inf / NaN dY the generic
+  // loop and the reference's autograd give NaN from 0 * Inf at a zero-weight tap; this path does not)
   int pok = 1;
   for (int e = tid; e < C * 27; e += kThreads) {
     const int f = (e % 27) / 9, tap = e % 9, tr = tap / 3, tc = tap % 3;
@@ -1364,7 +1360,8 @@ __global__ __launch_bounds__(kThreads) void gnca_b_dots(const BC2Args a) {
       if (!(mx > a.gthr)) continue;
     }
     const size_t q = (size_t)i * W + j, t = (size_t)it * W + j;
-    // a dead target adds exactly +0 (s = 0 + sum x * 0 for finite x): skipped
+    // a dead target adds exactly +0 (s = 0 + sum x * 0) for finite x: skipped (an Inf / NaN x here
+    // would give the reference's autograd NaN from Inf * 0; this shortcut assumes a finite state)
     if (a.keep && !a.keep[(size_t)b * HW + t]) continue;
     float s = a.dmb[(size_t)b * HW + t];
     for (int c = 0; c < C; ++c) s = fmaf(xb[c * HW + q], gb[c * HW + t], s);
@@ -1641,9 +1638,9 @@ static const BBSpec kBBS[] = {
 struct BwdPlan {
   FwdLayout F;
   const BBVariant* bb;
-  const void* bbfn;    // the BB kernel: gnca_b_split<MSG, true> (C = 16, hidden = 128) or bb->fn
-  const void* bbfn2;   // the kernel of slices after the first (gnca_b_split<MSG, false>, or bb->fn)
-  bool bbf32;          // BB is gnca_b_mlp (keep bytes, 16-byte staging), not the split A/B kernel
+  const void* bbfn;    // the BB kernel: bb->fn
+  const void* bbfn2;   // the kernel of slices after the first (bb->fn)
+  bool bbf32;          // BB is gnca_b_mlp (keep bytes, 16-byte staging): always, since round 6
   int CP, HB, nslices;
   bool graph, msg, zp, gn;
   int RY, RX;
@@ -1746,49 +1743,8 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
 #endif
   P->bbf32 = true;
   P->RXB = rxb;
-  // C = 16, hidden = 128: the split-arithmetic BB (gnca_bb_split.h), two 64-unit hidden slices (the
-  // per-wave weight-gradient accumulators of the whole hidden layer do not fit the register file),
-  // its own tile (the cheapest by the same makespan model within its LDS: weight images 28 KB + 4 x
-  // 16 KB wave scratch)
-  // Measured slower than the fp32-MFMA gnca_b_mlp at B=1024 72^2 (4.09 vs 3.24 ms for BB: stores of
-  // dY / dG and the per-tile staging stall its one wave per SIMD), so it is built only
-  // in A/B builds (-DGNCA_BB_SPLIT); the product backward runs gnca_b_mlp.
-#ifdef GNCA_BB_SPLIT
-  const bool split_bb = C == 16 && Hd == 128;
-  if (split_bb) {
-    double bestS = 1e300;
-    int sth = 0, stw = 0;
-    size_t slds = 0;
-    for (int th : ths)
-      for (int tw : tws) {
-        if ((th * tw) % 64 || tw + 2 * rx + 2 > 64) continue;
-        if (eth && (th != eth || tw != etw)) continue;
-        const BSLayout L = bs_layout(th, tw, ry, rx);
-        // + the kernel's static LDS (offset weights) and a margin
-        if ((size_t)L.total + GNCA_MAX_OFFSETS * 4 + 256 > 160 * 1024) continue;
-        const long tx = (W + tw - 1) / tw, ty = (H + th - 1) / th;
-        const long tiles = (long)d->B * tx * ty, cus = bwd_device_cus();
-        const long rounds = (tiles + cus - 1) / cus;
-        // per tile: its cells (in 32-cell groups) + the staged halo + a fixed part
-        const double per_tile = (double)th * tw + 0.01 * L.RH * L.RW * 16 + 60.0;
-        const double cost = (double)std::max<long>(rounds * cus, tiles) * per_tile;
-        if (cost < bestS) { bestS = cost; sth = th; stw = tw; slds = (size_t)L.total; }
-      }
-    if (sth) {
-      P->TH = sth;
-      P->TW = stw;
-      P->ldsB = slds;
-      P->bbfn = P->msg ? reinterpret_cast<const void*>(&gnca_b_split<true, true>)
-                       : reinterpret_cast<const void*>(&gnca_b_split<false, true>);
-      P->bbfn2 = P->msg ? reinterpret_cast<const void*>(&gnca_b_split<true, false>)
-                        : reinterpret_cast<const void*>(&gnca_b_split<false, false>);
-      P->HB = kBSHB;
-      P->nslices = 128 / kBSHB;
-      P->RXB = rx;   // its own staging (4-byte pieces, the unpadded halo)
-      P->bbf32 = false;
-    }
-  }
-#endif
+  // (a split-arithmetic BB on bf16 MFMA was built and measured slower, 4.09 vs 3.24 ms for BB at
+  // B=1024 72^2: DESIGN.md Appendix A.1; removed in round 6, it is in the git history)
   if (P->bbf32) {
   P->HB = P->bb->HB;
   P->nslices = (Hd + P->HB - 1) / P->HB;

@@ -87,6 +87,9 @@ __device__ __forceinline__ f32x16 mfma_bx(u32x4 a, u32x4 b, f32x16 c) {
                                                  c, 0, 0, 0);
 }
 
+// 16 zero bytes in global memory: the LDS-DMA source of the zero-padded shift's out-of-image quads
+__device__ __attribute__((aligned(16))) float gnca_zero16[4];
+
 #ifndef GNCA_K1_PIPE_LDS
 #define GNCA_K1_PIPE_LDS 1   // pipeline depth of the gather / perception reads (A/B builds: 0 = the plain loops)
 #endif
@@ -463,7 +466,11 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
   };
 
   // LDS-DMA staging of a tile's channel planes: 16-byte quads of every plane (torus-wrapped), lanes
-  // past the region masked off (the plane pads stay zero)
+  // past the region masked off (the plane pads stay zero).  ZP: a quad outside the image (a quad is
+  // inside or outside as a whole, W % TW == 0) stages zeros from gnca_zero16, so that the gather's
+  // product with its zero sender byte is an exact 0 as in _shift2d_pad (graph_augmentation.py:85-92),
+  // also for a non-finite x across the opposite border (exact by construction; not observable through
+  // a whole zero-pad step, whose pooled offset logits are NaN for any non-finite state)
   auto issue_dma = [&](int t, int w0, int wstep) {
     const int b = t / a.tps, tin = t - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
@@ -475,13 +482,15 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
       if (q < NQ) {
         const int e = 4 * q, vr = e / RW, vc = e - (e / RW) * RW;
         int ii = i0 - RY + vr, jj = j0 - RX + vc;
+        const bool outq = ZP && (ii < 0 || ii >= H || jj < 0 || jj >= W);
         ii = ii < 0 ? ii + H : (ii >= H ? ii - H : ii);
         jj = jj < 0 ? jj + W : (jj >= W ? jj - W : jj);
-        const float* src0 = xb + ii * W + jj;
+        const float* src0 = outq ? gnca_zero16 : xb + ii * W + jj;
+        const size_t cstr = outq ? 0 : HW;
         float* dst = xs + 256 * ii_;
 #pragma unroll 4
         for (int c = 0; c < C; ++c)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (size_t)c * HW),
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src0 + (size_t)c * cstr),
                                            (__attribute__((address_space(3))) void*)(dst + c * PSTR), 16, 0, 0);
       }
     }
@@ -1212,7 +1221,7 @@ __global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(con
 #pragma unroll
           for (int o = 0; o < KU; ++o) {
             const int d = a.odl[o];
-            const float s_ = (float)spq[-d];
+            const float s_ = ZP ? a.offw[(size_t)b * KU + o] * (float)spq[-d] : (float)spq[-d];
             S += s_;
             const float* xo = xq - d;
 #pragma unroll

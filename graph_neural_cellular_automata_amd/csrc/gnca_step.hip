@@ -243,7 +243,13 @@ __device__ __forceinline__ void fin_consts(float gam, float bet, float mu, float
 }
 
 // the update of one non-alpha value: (x + gain) + (-2 gain) / (2^(d sc + sh) + 1), g2 = -2 gain
+#ifndef GNCA_K2_ABL
+#define GNCA_K2_ABL 0   // timing-only A/B builds (wrong results): 1 = K2's main pass with a clamp for its two
+                        // transcendentals, 2 = its main pass a plain copy of x (no dx loads), 4 = K2's alpha
+                        // phase with a clamp for tanh (the states stay bounded, the live fraction similar)
+#endif
 __device__ __forceinline__ float k2_update(float x, float d, float sc, float sh, float gain, float g2) {
+  if (GNCA_K2_ABL & 1) return fmaf(g2, __builtin_amdgcn_fmed3f(fmaf(d, sc, sh), 0.f, 1.f), x + gain);
   return fmaf(g2, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(fmaf(d, sc, sh)) + 1.f), x + gain);
 }
 
@@ -259,6 +265,7 @@ __device__ __forceinline__ float fin_alpha(float xa, float d, float mu, float rs
 
 #include "gnca_k1_split.h"
 #include "gnca_k1_split32.h"
+
 
 namespace gnca {
 
@@ -1094,7 +1101,10 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
   const float g2 = -2.f * a.gain;
 
   // (3) updated alpha over band + halo, then the post-update alive mask (3x3 max-pool, -inf pad)
-  auto alpha_at = [&](float xa, float d) { return fin_alpha(xa, d, mu, rs, g3, b3, a.gain, gn); };
+  auto alpha_at = [&](float xa, float d) {
+    if (GNCA_K2_ABL & 4) return xa + __builtin_amdgcn_fmed3f(gn ? (d - mu) * rs * g3 + b3 : d, -1.f, 1.f) * a.gain;
+    return fin_alpha(xa, d, mu, rs, g3, b3, a.gain, gn);
+  };
   // compact field: K1 writes the alpha plane for live cells only; a dead cell's update is 0 (its
   // row's live mask, already in LDS for the band rows and the halo rows)
   auto live_at = [&](int e) {
@@ -1254,6 +1264,13 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
       // C4's shard B=128 72^2 0.0832 vs 0.0822 ms/step, c5 0.654 vs 0.653; profiles/r05f_ab_k2_alone.txt)
       for (int c0 = 0; c0 < C; c0 += CU) {
         vf xq[CU], fq[CU];
+        if (GNCA_K2_ABL & 2) {   // timing only: a copy of x
+#pragma unroll
+          for (int u = 0; u < CU; ++u)
+            if (c0 + u < C && c0 + u != 3)
+              *reinterpret_cast<vf*>(ob + (size_t)(c0 + u) * HW + p0) = *reinterpret_cast<const vf*>(xb + (size_t)(c0 + u) * HW + p0);
+          continue;
+        }
 #pragma unroll
         for (int u = 0; u < CU; ++u) {
           const int c = c0 + u;
@@ -1292,6 +1309,8 @@ __device__ __forceinline__ void k2_body(const K2Args& a, float* smem, float* sh_
 // (compact: 64 VGPRs with 2 channels in flight; round 3's 5 took 75 and a cap at 64 spilled)
 #ifdef GNCA_K2_MAXV   // A/B builds: a minimum of waves per SIMD (a VGPR cap), so that more K2 waves fit beside a K1
 #define GNCA_K2_ATTR __attribute__((amdgpu_waves_per_eu(GNCA_K2_MAXV)))
+#elif defined(GNCA_K2_NUMV)   // A/B builds: a VGPR cap of 2 x GNCA_K2_NUMV (gfx950 doubles amdgpu_num_vgpr: VGPRs + AGPRs)
+#define GNCA_K2_ATTR __attribute__((amdgpu_num_vgpr(GNCA_K2_NUMV)))
 #else
 #define GNCA_K2_ATTR
 #endif
@@ -1411,11 +1430,12 @@ struct K0Args {
 };
 
 // K0's first phase: the per-(channel, row) fp64 sums of x in the canonical order (canon_row_sums), one
-// workgroup per (channel, sample) so that a small batch still spreads over the chip (one workgroup per
-// sample took 57 us for B=16 40^2); a rollout's later steps take them from the previous step's K2
+// workgroup per (sample, channel) so that a small batch still spreads over the chip (one workgroup per
+// sample took 57 us for B=16 40^2); a rollout's later steps take them from the previous step's K2.
+// Samples on grid x (up to 2^31 - 1), channels on grid y (<= 65535)
 template <int V>
 __global__ __launch_bounds__(kThreads) void gnca_k0_rowsums(const float* x, double* rs, int C, int H, int W) {
-  const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int b = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
   const size_t HW = (size_t)H * W;
   canon_row_sums<V, 4>(x + ((size_t)b * C + c) * HW, H, W, rs + ((size_t)b * C + c) * H, tid >> 5, kThreads / 32,
                        tid & 31);
@@ -1609,6 +1629,7 @@ __global__ __launch_bounds__(kThreads) void gnca_fire_mask(uint8_t* mask, int B,
   }
 }
 
+#ifndef GNCA_K1_PROBE   // tools/k1_probe.sh: no host code (no instance table), for register / ISA studies
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
@@ -2016,10 +2037,11 @@ static int launch_k0(const gnca_step_desc* d, const gnca_weights* w, const Plan&
   double* rs = reinterpret_cast<double*>(ws + P.off_rs);
   k0.rs = rs;
   k0.B = d->B; k0.C = d->C; k0.H = d->H; k0.W = d->W; k0.d = d->d_model; k0.k = P.k;
-  if (d->B > 65535) return GNCA_ERR_UNSUPPORTED;   // (grid y)
-  if (!rows_ready)
-    hipLaunchKernelGGL((d->W & 3) == 0 ? gnca_k0_rowsums<4> : gnca_k0_rowsums<1>, dim3(d->C, d->B), dim3(kThreads),
+  if (!rows_ready) {
+    if (d->C > 65535) return GNCA_ERR_UNSUPPORTED;   // (grid y)
+    hipLaunchKernelGGL((d->W & 3) == 0 ? gnca_k0_rowsums<4> : gnca_k0_rowsums<1>, dim3(d->B, d->C), dim3(kThreads),
                        0, st, x, rs, d->C, d->H, d->W);
+  }
   for (int o = 0; o < 2 * P.k; ++o) k0.offs[o] = d->offsets[o];
   const size_t lds = ((size_t)d->C * d->H + d->C + d->d_model + P.k + (size_t)d->C * P.k +
                       (size_t)P.k * d->d_model) * sizeof(double) + 2 * (size_t)d->d_model * d->C * sizeof(float);
@@ -2680,3 +2702,5 @@ int gnca_rollout_stamped_f32(const gnca_step_desc* desc, const gnca_weights* w, 
 }
 
 }  // extern "C"
+
+#endif  // GNCA_K1_PROBE

@@ -159,7 +159,11 @@ int gnca_step_masked_f32(const gnca_step_desc* desc, const gnca_weights* w, cons
 #define GNCA_PHASE_ALL (GNCA_PHASE_K0 | GNCA_PHASE_K1 | GNCA_PHASE_K2)
 /* Rollout mode of the measurement hook: K2 writes the next step's alive masks into the workspace
  * and K1 reads them (what gnca_rollout_f32 does for every step after the first; needs
- * 0 <= alpha_thr <= graph_alpha_thr, and a K2 call with this bit on the same workspace first). */
+ * 0 <= alpha_thr <= graph_alpha_thr, and a K2 call with this bit on the same workspace first).
+ * On a zero-padded-shift graph step with GNCA_PHASE_COMPACT as well, that K2 also hands over the
+ * new state's per-(channel, row) sums and the next K0 reads them instead of recomputing them: both
+ * calls of such a pair must carry the same flags (a pair that mixes COMPACT and non-COMPACT calls
+ * would read stale sums). */
 #define GNCA_PHASE_ALIVE (1u << 3)
 /* Rollout mode's compact update field (what gnca_rollout_f32 does for every step when the planned
  * K1 is the 16-channel split kernel): K1 writes dx only for its live cells, packed per tile in

@@ -211,3 +211,25 @@ def bench_train_nccl(rank, world, port, q, root):
     except BaseException as exc:
         q.put({"error": f"{type(exc).__name__}: {exc}"})
         raise
+
+
+def bench_strong_gloo(rank, world, port, q, root):
+    """``bench.py --gpus 2 --scaling strong --dist-backend gloo --batch 256``: bench's own launcher
+    starts two ranks on the box's one GPU (a fixed global batch of 256 split 128 per rank, C4's
+    fixed-pool form), as a child process of this forkserver child; returns bench's JSON line."""
+    import json
+    import subprocess
+    import sys
+    try:
+        env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--scaling", "strong",
+                            "--dist-backend", "gloo", "--batch", "256", "--steps", "4", "--warmup", "1",
+                            "--gpu-warmup-ms", "0", "--no-cpu"],
+                           cwd=root, env=env, capture_output=True, text=True, timeout=100)
+        if r.returncode != 0:
+            q.put({"error": f"bench rc {r.returncode}: {r.stderr[-2000:]}"})
+            return
+        q.put({"line": json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])})
+    except BaseException as exc:
+        q.put({"error": f"{type(exc).__name__}: {exc}"})
+        raise

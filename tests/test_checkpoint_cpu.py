@@ -93,14 +93,13 @@ def test_sharded_pool_streams_resume_per_rank(tmp_path):
     before = other.rng_state()
     load_checkpoint(payload, _model(), pool=other)
     assert other.rng_state() == before
-    # an older checkpoint's single unlabelled stream is the saving rank's (rank 0): restored there
+    # an older checkpoint's single unlabelled stream (its world size not recorded, so the sharding
+    # may differ): every rank keeps its fresh stream
     old = dict(payload, pool_rng_state=live[0].rng_state())
-    expect0 = live[0].sample(3)[0]
     fresh = pools(2)
     for p in fresh:
         load_checkpoint(old, _model(), pool=p)
-    assert fresh[0].sample(3)[0] == expect0
-    assert fresh[1].rng_state() == pools(2)[1].rng_state()
+    assert [p.rng_state() for p in fresh] == [p.rng_state() for p in pools(2)]
 
 
 def _pool_ckpt_rank(rank, world, port, path, q):

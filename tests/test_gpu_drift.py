@@ -47,6 +47,12 @@ CASES = {
     # the fp32-MFMA runtime K1 before)
     "graph_zeropad_split8x24": ("graph_zeropad_latest_grown_b1_72", True, 16, 72, 8, 4, 8, 96, (0, 7),
                                 "gnca_k1_split<8,24,4,4,8>", False, True),
+    # the zero-pad LARGE-batch plan (what bench --config zeropad times): the ZP instance
+    # of the 24x36 split K1 fed K0's per-sample offset weights, the compact update field, two
+    # sub-batch streams, and K2 handing the next step's K0 the new state's row sums (B=192: two
+    # sub-batches of 96 samples = 576 tiles each, above the compact field's 2 per CU)
+    "graph_zeropad_split24x36": ("graph_zeropad_latest_grown_b1_72", True, 16, 72, 192, 4, 8, 32, (0, 96, 191),
+                                 "gnca_k1_split<24,36,4,4,8>", True, True, 2),
 }
 ARITH = {}   # every case: bf16x6 (the split K1s)
 # every case's max |hip - f64| is appended here (JSON lines; the GPU box merges gpurun_out/ back)
@@ -68,6 +74,7 @@ def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
     from graph_neural_cellular_automata_amd import step as S
     fx, graph, C, H, B, R, K, T, check, k1_expected, compact, *rest = CASES[case]
     zp = bool(rest and rest[0])
+    subs = rest[1] if len(rest) > 1 else None   # the sub-batch streams the rollout must plan
     c = Case(fx)
     p64 = {k: v.astype(np.float64) for k, v in c.weights.items()}
     wt = {k: torch.from_numpy(np.ascontiguousarray(v.astype(np.float32))).to(dev) for k, v in c.weights.items()}
@@ -96,6 +103,8 @@ def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
     name, arith = S.k1_variant(d)
     assert (name, arith) == (k1_expected, ARITH.get(case, "bf16x6"))
     assert S.rollout_compact(d) == compact, "the rollout's update-field layout"
+    if subs is not None:
+        assert S.rollout_subs(d) == subs, "the rollout's sub-batch streams"
     got = S.rollout(d, w, x.contiguous(), T, offs).cpu().numpy()
     assert np.isfinite(got).all()
     cfg = dict(update_gain=GAIN, alpha_thr=THR, use_groupnorm=True, graph=graph, message_gain=MSG,
@@ -111,6 +120,7 @@ def test_shipping_rollout_drift_vs_f64_oracle(dev, case):
     os.makedirs(os.path.dirname(DRIFT_LOG), exist_ok=True)
     with open(DRIFT_LOG, "a") as f:
         f.write(json.dumps({"case": case, "k1": name, "compact": compact, "fold": S.rollout_fold(d), "zero_pad": zp,
+                            "sub_batches": S.rollout_subs(d),
                             "batch": B, "canvas": H, "steps": T, "samples": list(check),
                             "max_abs_err_vs_f64": err, "mean_abs_err_vs_f64": float(np.abs(got[idx] - ref).mean()),
                             "alive_flips": flips, "tolerance": 1e-4, "time": time.time()}) + "\n")

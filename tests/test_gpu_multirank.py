@@ -153,3 +153,18 @@ def test_rccl_world1_train_bench(dev):
     # gate_mlp never gets one)
     assert 0 < line["allreduce_bytes"] <= 4 * 10753 and line["allreduce_bytes"] % 4 == 0
     assert np.isfinite(line["final_loss"])
+
+
+def test_bench_strong_scaling_two_ranks_one_gpu(dev):
+    """``bench.py --scaling strong --gpus 2``: C4's fixed pool (here 256 samples) split over two ranks
+    (both on the box's one GPU, gloo), so the driver's 1 -> 8 GPU run can measure a fixed global batch
+    beside the weak-scaling default; the line reports the global batch and each rank's share."""
+    from tests import mr_workers as M
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    line = _run_one(M.bench_strong_gloo, (root,), timeout=115)["line"]
+    print(f"[multirank] strong-scaling bench, 2 ranks: {line['value']:.3e} cell-upd/s")
+    assert line["scaling"] == "strong" and line["n_gpus"] == 2 and line["ranks_seen"] == 2
+    assert line["config"]["global_batch"] == 256 and line["config"]["batch_per_gpu"] == 128
+    assert len(line["rank_state_checksums"]) == 2 and all(np.isfinite(line["rank_state_checksums"]))
+    assert line["value"] == pytest.approx(256 * 72 * 72 * line["steps"] / (line["ms_per_step"] * line["steps"] / 1e3),
+                                          rel=1e-6)
