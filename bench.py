@@ -70,7 +70,12 @@ WORKLOADS = {
 # (tools/pmc.sh + tools/pmc_traffic.py); counters cannot be read from inside this process
 # the passes of the shipped build (round 4's final tag r04h; a round's tags are not in time order, so
 # the name is explicit), else the highest-named file
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05z_pmc_traffic.json")
+# round 6: the passes of the final build (tools/_s6z.sh) carry the sha256 of the libgnca.so they ran
+# (lib_sha16); the line reports whether that is the library this run loaded ("pmc_build_match")
+PMC_TAG = os.environ.get("GNCA_PMC_TAG", "r06z")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", f"{PMC_TAG}_pmc_traffic.json")
+if not os.path.exists(PMC_TRAFFIC):
+    PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05z_pmc_traffic.json")
 if not os.path.exists(PMC_TRAFFIC):
     PMC_TRAFFIC = max(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc_traffic.json")) or
                       [os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")])
@@ -87,8 +92,35 @@ def pmc_file(config):
     profiles/r05_pmc_traffic_<config>.json (tools/pmc.sh with BENCH_ARGS="--config <config>"), or None."""
     if config == "headline":
         return PMC_TRAFFIC
-    f = os.path.join(ROOT, "profiles", f"r05_pmc_traffic_{config}.json")
-    return f if os.path.exists(f) else None
+    for f in (os.path.join(ROOT, "profiles", f"{PMC_TAG}_pmc_traffic_{config}.json"),
+              os.path.join(ROOT, "profiles", f"r05_pmc_traffic_{config}.json")):
+        if os.path.exists(f):
+            return f
+    return None
+
+
+def lib_sha16(path):
+    """First 16 hex digits of the sha256 of a built library (the build a measurement ran)."""
+    import hashlib
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def pmc_provenance(config, loaded_lib):
+    """Which committed PMC passes the line's traffic / MFMA-busy numbers come from, and whether they
+    were collected with the very library this run loaded."""
+    f = pmc_file(config)
+    if f is None:
+        return None
+    try:
+        src = json.load(open(f)).get("lib_sha16")
+    except Exception:
+        src = None
+    here = lib_sha16(loaded_lib)
+    return {"file": os.path.relpath(f, ROOT), "pmc_lib_sha16": src, "this_run_lib_sha16": here,
+            "pmc_build_match": bool(src) and src == here}
 
 
 def pmc_traffic(kernel, config="headline"):
@@ -713,7 +745,7 @@ def main():
     #     where every K1 / K2 workgroup writes wall-clock stamps (100 MHz s_memrealtime) at its start
     #     and end: a launch's duration is max(end) - min(start), with nothing inserted in the stream
     #     between launches.  The stamped run's own wall time is reported beside the timed one. ---
-    if not torch.equal(dst2.view(torch.int32), out.view(torch.int32)):
+    if not torch.equal(dst2.view(torch.int32), out.view(torch.int32)) and not os.environ.get("GNCA_AB_TIMING_ONLY"):
         raise SystemExit("bench: the stamped rollout differs from the timed rollout")
     sv = stamps.view(args.steps, nsub, 2, cap, 2).cpu().numpy()
     dur = np.zeros((args.steps, nsub, 2))
@@ -831,9 +863,12 @@ def main():
     k1_s = k1_ms * 1e-3
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     k1_key = "K1F" if fold else "K1"      # the PMC passes' name for the timed K1 (tools/pmc_traffic.py)
-    pmc_busy = pmc_mfma_busy(k1_key, cus, args.config)
-    k1_traffic = pmc_traffic(k1_key, args.config)
-    pmc_src = pmc_file(args.config)
+    # the PMC passes of this workload: the config's, or for a non-default batch their own (e.g. C4's
+    # 128-sample shard: profiles/<tag>_pmc_traffic_b128.json)
+    pmc_key = args.config if B == wl["B"] else (f"b{B}" if args.config == "headline" else f"{args.config}_b{B}")
+    pmc_busy = pmc_mfma_busy(k1_key, cus, pmc_key)
+    k1_traffic = pmc_traffic(k1_key, pmc_key)
+    pmc_src = pmc_file(pmc_key)
     roof = {"bound": "mfma", "kernel": k1_name[:-1] + ",fold>" if fold else k1_name, "arith": arith,
             "achieved": live_flops / k1_s / 1e12,
             "peak": peak_eq / 1e12, "unit": "TFLOP/s",
@@ -870,7 +905,7 @@ def main():
                "k2_launches_timed": 1 if fold else launches * nsub,
                "note": ("the fold: K2 runs once per rollout (after its last step); every other step's "
                         "finish is inside the next step's K1") if fold else None,
-               "traffic": pmc_traffic("K2", args.config)}
+               "traffic": pmc_traffic("K2", pmc_key)}
 
     if rank == 0:
         cpu = None
@@ -903,6 +938,7 @@ def main():
                                 "k1_ms": k1_ms, "k2_ms": k2_ms,
                                 "gaps_minus_overlap_ms_per_step": span_ms - k1_ms - k2_ms},
             "roofline": roof, "roofline_k2": roof_k2, "cpu_baseline": cpu,
+            "pmc_provenance": pmc_provenance(pmc_key, L.LIB_PATH),
         }
         print(json.dumps(line), flush=True)
     if world > 1 or args.pg1:

@@ -337,10 +337,6 @@ __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst)
 #define GNCA_K1_SPLIT_NT 512   // threads per workgroup of the 16-channel split K1 (768: 3 waves per SIMD)
 #endif
 
-#ifndef GNCA_K1_NOBAR
-#define GNCA_K1_NOBAR 1   // the large tiles' K1 without the end-of-tile barrier (A/B builds: 0 = the barrier)
-#endif
-
 #ifndef GNCA_K1_PRIO
 #define GNCA_K1_PRIO 1   // wave issue priority of K1's groups (s_setprio): below K2's (GNCA_K2_PRIO = 3) so that a
                          // co-resident K2 issues its loads first (round 4: 2 -> 1 with K2 at 3, step 0.4995 -> 0.4912 ms)
@@ -367,9 +363,6 @@ __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst)
 #ifdef GNCA_K1_MAXVGPR   // A/B builds: a VGPR cap below the occupancy's (room for a co-resident K2 wave)
 #define GNCA_K1_VATTR __attribute__((amdgpu_num_vgpr(GNCA_K1_MAXVGPR)))
 #else
-// the large tiles' K1 (the sub-batch pipeline): at most 192 VGPRs, so that two 64-VGPR K2 waves fit
-// beside its two waves on a SIMD (gfx950 reads amdgpu_num_vgpr(n) as n VGPRs + n AGPRs: 96 -> 192;
-// the barrier-free tile loop came out at 194 uncapped, 192 with one spill outside the group loop)
 #define GNCA_K1_VATTR
 #endif
 
@@ -380,7 +373,7 @@ __global__ __launch_bounds__(512) void gnca_ks_images(const K1Args a, char* dst)
 // ZP: the zero-padded shift (graph_augmentation.py's zero_padded_shift): per-sample offset weights
 // from K0 and no sender outside the image (the torus-wrapped staging there is multiplied by 0)
 template <int TH, int TW, int RY, int RX, int KU, int FOLD = 0, bool ZP = false>
-__device__ __forceinline__ void ks_k1_body(const K1Args& a) {
+__global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(const K1Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_b[];
   constexpr int C = 16, HD = 128, NT = GNCA_K1_SPLIT_NT, NW = NT / 64;
   constexpr int RH = TH + 2 * RY, RW = TW + 2 * RX, RHW = RH * RW;
@@ -461,50 +454,6 @@ __device__ __forceinline__ void ks_k1_body(const K1Args& a) {
   const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
   const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
   const int t_begin = xg_ * tq + min(xg_, trm), t_end = (GNCA_ABLATE & kAblTiles) ? t_begin : t_begin + tq + (xg_ < trm ? 1 : 0);
-
-  // Dynamic tiles (a.tctr, rollouts): a workgroup's first tile is static (t_begin + xr_), every later
-  // one is claimed from its XCD group's counter by the preparer wave at the top of the current tile
-  // (one atomic per tile) and published to the other waves through LDS (cnt[6 + par], cnt[9] =
-  // claims published): a workgroup that is ahead takes the next tile, so a launch does not end on the
-  // one workgroup that was handed one tile more than its neighbours.  Tiles stay contiguous per XCD
-  // (its L2 keeps the halo re-reads).  Which workgroup runs a tile does not change any result.
-  // The non-fold K1 always takes this path (one code path: a runtime choice between it and the
-  // fold's uniform next-tile computation cost 11 VGPRs); without counters (single steps, masked
-  // steps) the preparer publishes the static next tile instead of a claimed one.
-  constexpr bool dyn = FOLD == 0;
-  // NOBAR (the large tiles' plain K1): no workgroup barrier between tiles.  A wave that has run out of
-  // groups goes on to the next tile as soon as that tile is staged and prepared, instead of waiting
-  // for the other waves' last MFMA chains (a third of a tile's 14 groups are in flight at its end: the
-  // end-of-tile barrier held every wave ~17 % of K1, profiles/r06_pipe_prof.txt).  LDS state per tile
-  // parity p (group and staged-read counters cnt[2 + 2p] / cnt[3 + 2p] with per-wave bases) and
-  // sequence flags: cnt[8] tiles staged, cnt[10] tiles prepared, cnt[11] tile entries (NW per tile).
-  //   entry of tile t (t > 0): wait staged > t and prepared > t; count the entry
-  //   preparer: claim / publish t + 1; wait until every wave entered t (slot p^1 and the other
-  //             per-parity state of t - 1 are free); prepare t + 1 into slot p^1; prepared = t + 2
-  //   first failing pull: wait for every group's staged reads, stage t + 1; staged = t + 2
-  //   last failing pull (every group of t complete): the tile's GroupNorm bins
-  // Every wait is on work that needs no wave that waits (no cycle).  Same arithmetic, same bits.
-  constexpr bool NOBAR = GNCA_K1_NOBAR && FOLD == 0 && !SMALLT;
-  auto claim_publish = [&](int it, int pp, int cur) {   // wave PW: the next tile (t_end: none), published
-    int n = t_end;
-    if (lane == 0) {
-      n = a.tctr ? t_begin + per_x + atomicAdd(a.tctr + xg_, 1) : cur + per_x;
-      // (masked steps, static tiles only: an inactive sample's tiles get zero GroupNorm partials)
-      while (n < t_end && a.active && !a.active[n / a.tps]) {
-        for (int e = 0; e < 2 * NW; ++e) a.stats[(size_t)n * 2 * NW + e] = 0.0;
-        n += per_x;
-      }
-      n = min(n, t_end);
-      cnt[6 + pp] = n;
-      __hip_atomic_store(cnt + 9, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    return __builtin_amdgcn_readfirstlane(n);   // (lane 0's: wave-uniform, an SGPR)
-  };
-  auto wait_next = [&](int it, int pp) {   // another wave: the next tile the preparer claimed
-    while (__hip_atomic_load(cnt + 9, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= it)
-      __builtin_amdgcn_s_sleep(1);
-    return __builtin_amdgcn_readfirstlane(cnt[6 + pp]);
-  };
 
   // the next active tile of this workgroup's sequence after `t` (inactive samples of a masked step
   // get zero GroupNorm partials and no work)
@@ -1145,11 +1094,7 @@ __device__ __forceinline__ void ks_k1_body(const K1Args& a) {
   ARR_MARK(1);
   float pcv = 0.f;
   if (!a.wimg && tid < C * 27) pcv = a.perc[tid];
-  if (tid == 0) {
-    *gctr = 0; *xsd = 0;
-    if (!FOLD) cnt[9] = 0;
-    if (NOBAR) { cnt[4] = 0; cnt[5] = 0; cnt[8] = 1; cnt[10] = 1; cnt[11] = 0; }
-  }
+  if (tid == 0) { *gctr = 0; *xsd = 0; }
   if (!(GNCA_ABLATE & kAblFill)) {
     if (a.wimg) {
       // the rollout's weight images, built once (gnca_ks_images): one LDS-DMA copy of the block (the
@@ -1221,19 +1166,9 @@ __device__ __forceinline__ void ks_k1_body(const K1Args& a) {
   // compaction run on the preparer wave beside the other waves' groups instead of between them.
   int par = 0;
   int iter = 0;
-  int gb_o = 0, xb_o = 0;   // NOBAR: the other parity's counter bases (this tile's: gbase / xbase, swapped per tile)
   while (tile < t_end) {
     PROF_MARK(7);
-    if constexpr (NOBAR) {
-      if (iter > 0)   // (tile 0: the prologue's barrier)
-        while (__hip_atomic_load(cnt + 8, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= iter ||
-               __hip_atomic_load(cnt + 10, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= iter)
-          __builtin_amdgcn_s_sleep(1);
-      if (lane == 0) __hip_atomic_fetch_add(cnt + 11, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      PROF_MARK(6);   // (NOBAR: the wait for the tile's staging / preparation)
-    }
-    // (dyn: only the preparer wave knows the next tile here; the others read it when they need it)
-    const int nxt = dyn ? (wave == PW ? claim_publish(iter, par, tile) : t_end) : next_active(tile + per_x);
+    const int nxt = next_active(tile + per_x);
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
@@ -1243,28 +1178,14 @@ __device__ __forceinline__ void ks_k1_body(const K1Args& a) {
     const uint16_t* lst = reinterpret_cast<const uint16_t*>(smem_b + L.lst + par * L.lst_slot);
     const int nlive = cnt[par];
 
-    if (wave == PW && nxt < t_end && !(GNCA_ABLATE & kAblPrep)) {
-      if constexpr (NOBAR) {   // slot par^1 (tile t - 1's) is free once every wave entered this tile
-        while (__hip_atomic_load(cnt + 11, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NW * (iter + 1))
-          __builtin_amdgcn_s_sleep(1);
-      }
-      prep(nxt, par ^ 1, false, false);
-      if (NOBAR && lane == 0) __hip_atomic_store(cnt + 10, iter + 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    if (wave == PW && nxt < t_end && !(GNCA_ABLATE & kAblPrep)) prep(nxt, par ^ 1, false, false);
     PROF_MARK(3);   // preparer
 
     // ---- 32-cell groups, pulled from an LDS counter (the faster, older wave of a SIMD takes more);
     //      each group's GroupNorm partials go to pg[q], so the sums do not depend on which wave ran it ----
     const int qend = (nlive + 31) >> 5;
     double* pg = reinterpret_cast<double*>(smem_b + L.pg) + par * 2 * NG;
-    int* const gcp = NOBAR ? cnt + 2 + 2 * par : gctr;   // this tile's group / staged-read counters
-    int* const xcp = NOBAR ? cnt + 3 + 2 * par : xsd;
-    const int gb_ = gbase, xb_ = xbase;
-    auto pull = [&]() {
-      // (NOBAR: the group's partials / stores before the pull: the tile's last puller reads pg)
-      if (NOBAR) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      return (__builtin_amdgcn_readfirstlane(atomicAdd(gcp, 1)) >> 6) - gb_;
-    };
+    auto pull = [&]() { return (__builtin_amdgcn_readfirstlane(atomicAdd(gctr, 1)) >> 6) - gbase; };
     const bool img_top = i0 == 0, img_bot = i0 + TH == H, img_lft = j0 == 0, img_rgt = j0 + TW == W;
     // (every lane adds 1: the wave's 64 increments are one LDS instruction, so the counter moves by
     //  64 per pull and any lane's old value >> 6 is the pulled group)
@@ -1403,7 +1324,7 @@ __device__ __forceinline__ void ks_k1_body(const K1Args& a) {
       split3_x8(y1, yf[1][0], yf[1][1], yf[1][2]);
       split3_x8(y2, yf[2][0], yf[2][1], yf[2][2]);
       // this group's reads of the staged planes are done (release: they stay before the count)
-      __hip_atomic_fetch_add(xcp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(xsd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if constexpr (FOLD) __hip_atomic_fetch_or(cnt + 6 + par, 1 << q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       PROF_MARK(2);   // pull + gather + perception + splits
       if (GNCA_K1_DYNPRIO > 0) __builtin_amdgcn_s_setprio(GNCA_K1_PRIO + GNCA_K1_DYNPRIO);
@@ -1768,39 +1689,14 @@ __device__ __forceinline__ void ks_k1_body(const K1Args& a) {
     if constexpr (FOLD) {
       // every wave: the next tile's region finalized into the staging buffer (+ its cells into xo)
       if (nxt < t_end) finalize(nxt, par ^ 1, iter + 2, true, qend, lst, par);
-    } else if (q >= qend + nz && q < qend + nz + (NOBAR ? 1 : GNCA_DMA_WAVES)) {
-      const int nd = (dyn && wave != PW) ? wait_next(iter, par) : nxt;
-      if (nd < t_end) {
-        while ((__hip_atomic_load(xcp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xb_ < qend)
-          __builtin_amdgcn_s_sleep(1);
-        issue_dma(nd, q - qend - nz, NOBAR ? 1 : GNCA_DMA_WAVES);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      if (NOBAR && lane == 0) __hip_atomic_store(cnt + 8, iter + 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if (q >= qend + nz && q < qend + nz + GNCA_DMA_WAVES && nxt < t_end) {
+      while ((__hip_atomic_load(xsd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 6) - xbase < qend)
+        __builtin_amdgcn_s_sleep(1);
+      issue_dma(nxt, q - qend - nz, GNCA_DMA_WAVES);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     PROF_MARK(0);
     if (iter == 0) ARR_MARK(5);
-    if constexpr (NOBAR) {
-      {   // this parity's bases advance; the other parity's become current
-        const int g2 = gbase + qend + nz + NW, x2 = xbase + qend;
-        gbase = gb_o; xbase = xb_o; gb_o = g2; xb_o = x2;
-      }
-      // the tile's last puller: every group of the tile is complete (each wave pulls again only after
-      // its group's partials): the GroupNorm bins, as the barrier version's threads 0..15
-      if (q == qend + nz + NW - 1) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        int ln = lane;
-        asm volatile("" : "+v"(ln));   // (keeps the bins' addressing from being hoisted above the group loop)
-        if (ln < 2 * NW) {
-          double s_ = 0.0;
-          for (int q2 = ln >> 1; q2 < qend; q2 += NW) s_ += pg[2 * q2 + (ln & 1)];
-          a.stats[(size_t)tile * 2 * NW + ln] = s_;
-        }
-      }
-      PROF_MARK(5);   // per-tile reduction
-      // (slot par of cnt[6 + par] is rewritten two tiles on, after every wave entered the next tile)
-      tile = wave == PW ? nxt : wait_next(iter, par);
-    } else {
     __syncthreads();   // groups done, next tile staged, pg complete, slot par^1 ready
     PROF_MARK(6);
     if (iter == 0) ARR_MARK(6);
@@ -1815,43 +1711,14 @@ __device__ __forceinline__ void ks_k1_body(const K1Args& a) {
       a.stats[(size_t)tile * 2 * NW + tid] = s_;
     }
     PROF_MARK(5);   // per-tile reduction
-    // (dyn: slot par is rewritten two tiles on, after the next barrier, which every wave passes only
-    //  after this read)
-    tile = dyn ? __builtin_amdgcn_readfirstlane(cnt[6 + par]) : nxt;
-    }
+    tile = nxt;
     par ^= 1;
     ++iter;
-  }
-  // dyn: the XCD group's last workgroup to finish resets its counters for the next launch (every
-  // workgroup of the group made its last claim before its last barrier)
-  if (dyn && a.tctr && tid == 0) {
-    const int per_grp = per_x;
-    if (atomicAdd(a.tctr + 8 + xg_, 1) == per_grp - 1) {
-      __hip_atomic_store(a.tctr + xg_, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a.tctr + 8 + xg_, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
   PROF_STORE_W03;
   FPROF_STORE;
   ARR_MARK(7);
   GNCA_STAMP_END(a.stamps);
-}
-
-template <int TH, int TW, int RY, int RX, int KU, int FOLD = 0, bool ZP = false>
-__global__ __launch_bounds__(GNCA_K1_LB, 1) GNCA_K1_VATTR void gnca_k1_split(const K1Args a) {
-  ks_k1_body<TH, TW, RY, RX, KU, FOLD, ZP>(a);
-}
-
-// The large tiles' K1 (the sub-batch pipeline): at most 192 VGPRs, so that two 64-VGPR K2 waves fit
-// beside its two waves on a SIMD (gfx950 reads amdgpu_num_vgpr(n) as n VGPRs + n AGPRs: 96 -> 192).
-// The barrier-free tile loop came out at 194 uncapped; capped, it keeps one spill outside the groups.
-#ifndef GNCA_K1_CAP
-#define GNCA_K1_CAP 96
-#endif
-template <int TH, int TW, int RY, int RX, int KU, int FOLD = 0, bool ZP = false>
-__global__ __launch_bounds__(GNCA_K1_LB, 1) __attribute__((amdgpu_num_vgpr(GNCA_K1_CAP)))
-void gnca_k1_split_v192(const K1Args a) {
-  ks_k1_body<TH, TW, RY, RX, KU, FOLD, ZP>(a);
 }
 
 }  // namespace gnca

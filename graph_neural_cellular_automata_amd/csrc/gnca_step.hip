@@ -190,10 +190,6 @@ struct K1Args {
   uint32_t flags;
   uint64_t* stamps;    // measurement only (null in product launches): per-workgroup wall-clock stamps
   const char* wimg;    // split K1: the weight images built once per rollout (gnca_ks_images), or null
-  // split K1 in a rollout (no fold, no active mask): per-XCD tile claim counters [0..7] and their
-  // workgroups' done counts [8..15] (zeroed by the rollout before its first K1; each launch's last
-  // workgroup of an XCD group resets its pair), or null: the static tile split
-  int* tctr;
   // The fold (rollout mode, gnca_k1_split<..., FOLD = true>): this launch also FINISHES the previous
   // step.  Each tile's staged region is x = finalize(xp, dxp) (GroupNorm with the previous step's
   // partials, tanh * gain, residual, post-update alpha gate: K2's arithmetic) instead of an LDS-DMA
@@ -1653,25 +1649,18 @@ struct Variant {
 
 template <int TH, int TW, int RY, int RX, int KU>
 constexpr const void* ks_zp_fn() {
-  if constexpr (KU > 0 && TH * TW > 256) return reinterpret_cast<const void*>(&gnca_k1_split_v192<TH, TW, RY, RX, KU, 0, true>);
-  else if constexpr (KU > 0) return reinterpret_cast<const void*>(&gnca_k1_split<TH, TW, RY, RX, KU, 0, true>);
+  if constexpr (KU > 0) return reinterpret_cast<const void*>(&gnca_k1_split<TH, TW, RY, RX, KU, 0, true>);
   else return nullptr;
-}
-// the plain K1 of a tile shape: the large tiles' capped at 192 VGPRs (gnca_k1_split_v192)
-template <int TH, int TW, int RY, int RX, int KU>
-constexpr const void* ks_fn() {
-  if constexpr (TH * TW > 256) return reinterpret_cast<const void*>(&gnca_k1_split_v192<TH, TW, RY, RX, KU>);
-  else return reinterpret_cast<const void*>(&gnca_k1_split<TH, TW, RY, RX, KU>);
 }
 
 #define GNCA_GV(cp, hd) {cp, hd, 0, 0, 0, 0, 0, reinterpret_cast<const void*>(&gnca_k1_update<cp, hd, 0, 0, 0, 0, 0>), kThreads, 0, 0, {nullptr, nullptr}, 0, nullptr}
 #define GNCA_SV(th, tw, ry, rx, ku) \
-  {16, 128, th, tw, ry, rx, ku, ks_fn<th, tw, ry, rx, ku>(), GNCA_K1_SPLIT_NT, 1, \
+  {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
    ks_layout<th, tw, ry, rx>().total, {nullptr, nullptr}, 0, ks_zp_fn<th, tw, ry, rx, ku>()}
 // fold variants: the large-batch tile (dense: nullptr, it is only planned with the compact field) and
 // the small-batch ones (both layouts)
 #define GNCA_SVF(th, tw, ry, rx, ku, dense) \
-  {16, 128, th, tw, ry, rx, ku, ks_fn<th, tw, ry, rx, ku>(), GNCA_K1_SPLIT_NT, 1, \
+  {16, 128, th, tw, ry, rx, ku, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku>), GNCA_K1_SPLIT_NT, 1, \
    ks_layout<th, tw, ry, rx>().total, {dense, reinterpret_cast<const void*>(&gnca_k1_split<th, tw, ry, rx, ku, 2>)}, \
    ks_layout<th, tw, ry, rx, true>().total, ks_zp_fn<th, tw, ry, rx, ku>()}
 #define GNCA_S32V(th, tw, ry, rx, ku) \
@@ -1725,7 +1714,7 @@ struct Plan {
   int band_c, nbands_c, total2_c;   // K2 on the compact update field
   size_t lds2_c;
   // workspace carve (bytes)
-  size_t off_dx, off_stats, off_mm, off_offw, off_rs, off_alive, off_rmask, off_rpre, off_dxa, off_wimg, off_tctr, ws_bytes;
+  size_t off_dx, off_stats, off_mm, off_offw, off_rs, off_alive, off_rmask, off_rpre, off_dxa, off_wimg, ws_bytes;
   bool compact_ok;   // the rollout's compact update field (the bf16-split K1s, large batches)
   // the fold (rollouts of a fold-capable K1 on the compact field): K1 of step t also finishes step
   // t - 1, so the compact field (dx, row tables, alpha plane, partials) is double-buffered by the
@@ -1895,7 +1884,6 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   P->off_dxa = carve(P->compact_ok ? (size_t)d->B * d->H * d->W * sizeof(float) : 0);
   // the rollout's weight images of the 16-channel split K1 (built once per rollout, gnca_ks_images)
   P->off_wimg = carve(P->var->split == 1 ? (size_t)(ks_layout<24, 36, 4, 4>().total - ks_layout<24, 36, 4, 4>().w1) : 0);
-  P->off_tctr = carve(P->var->split == 1 ? 16 * sizeof(int) : 0);   // the split K1's tile counters
   // the fold: a fold-capable K1 on the compact field, thresholds that allow the alive hand-over
   // (0 <= alpha_thr <= graph_alpha_thr), 32-bit packed-field offsets; the second set of
   // the compact field (each field + 256 B: the finalizer's quad reads may touch one float past it)
@@ -2118,10 +2106,8 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
                      uint32_t phases = GNCA_PHASE_ALL, const uint8_t* active = nullptr,
                      bool alive_in = false, bool alive_out = false, bool compact = false,
                      uint64_t* stamps = nullptr, int stamp_cap = 0, const char* wimg = nullptr, int set = 0,
-                     bool k2_co = false, bool dyn_tiles = false) {
+                     bool k2_co = false) {
   // k2_co: this step's K2 runs beside another sub-batch stream's K1 (the rollout's sub-batch pipeline)
-  // dyn_tiles: the split K1 claims its tiles from the workspace's per-XCD counters (a rollout, which
-  // zeroed them on this stream before its first step)
   Plan P;
   if (!make_plan(d, false, &P)) {
     if (d && d->C >= 4 && d->hidden > 0 && !find_variant(d->C, d->hidden)) return GNCA_ERR_UNSUPPORTED;
@@ -2181,7 +2167,6 @@ static int step_impl(const gnca_step_desc* d, const gnca_weights* w, const float
   // measurement: K1's workgroups stamp into stamps[0 .. 2*cap), K2's into stamps[2*cap .. 4*cap)
   k1.stamps = stamps;
   k1.wimg = P.var->split == 1 ? wimg : nullptr;
-  k1.tctr = (dyn_tiles && P.var->split == 1 && !active) ? reinterpret_cast<int*>(wsb + P.off_tctr) : nullptr;
   if (stamps && (long)std::min<long>((long)device_cus() * occupancy(P.k1fn, P.lds1, P.var->NT),
                                      P.total_tiles) > stamp_cap)
     return GNCA_ERR_INVALID;
@@ -2301,9 +2286,6 @@ namespace gnca {
 // ---------------------------------------------------------------------------------------------
 #ifndef GNCA_ROLLOUT_IMAGES
 #define GNCA_ROLLOUT_IMAGES 1   // measurement builds: 0 = every K1 launch builds its weight images
-#endif
-#ifndef GNCA_K1_DYN_TILES
-#define GNCA_K1_DYN_TILES 0   // the split K1 claims its tiles from per-XCD counters (A/B builds only)
 #endif
 #ifndef GNCA_ROLLOUT_SUBS
 #define GNCA_ROLLOUT_SUBS 2   // measurement builds: 1 = one stream (no sub-batch pipeline)
@@ -2633,16 +2615,7 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
                      false, out_last, true, stamps ? stamps + (size_t)(T - 1) * 4 * stamp_cap : nullptr, stamp_cap,
                      wimg, (int)(dt.rng_step & 1));
   }
-  // the split K1's per-XCD tile counters: zero on each stream before its first K1 of this call (every
-  // launch leaves them zero again; a continuation piece zeroes them once more, in stream order)
-  // (measured, round 6: 1.2 % slower at the headline and the launch tail unchanged, 0.09-0.11 of a K1
-  //  launch's span against 0.09-0.10 static, profiles/r06_ab_dyn_tiles.txt: the static split is kept;
-  //  -DGNCA_K1_DYN_TILES=1 builds the claims for A/B runs)
-  const bool dyn = GNCA_K1_DYN_TILES && !fold;
   if (nsub == 1) {
-    if (dyn && PF.var->split == 1 && ws && ws_bytes >= PF.ws_bytes &&
-        hipMemsetAsync(reinterpret_cast<char*>(ws) + PF.off_tctr, 0, 16 * sizeof(int), st) != hipSuccess)
-      return GNCA_ERR_HIP;
     const float* src = x;
     for (int t = 0; t < steps; ++t) {
       float* dst = ((steps - 1 - t) % 2 == 0) ? x_final : scratch;
@@ -2650,8 +2623,7 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
       if ((desc->flags & GNCA_GRAPH) && k > 0) memcpy(dt.offsets, offsets + (size_t)t * 2 * k, 2 * k);
       const int rc = step_impl(&dt, w, src, dst, nullptr, nullptr, ws, ws_bytes, st, GNCA_PHASE_ALL,
                                nullptr, hand_alive && (t > 0 || in0), hand_alive && (t + 1 < steps || out_last),
-                               true, stamps ? stamps + (size_t)t * 4 * stamp_cap : nullptr, stamp_cap, wimg, 0,
-                               false, dyn);
+                               true, stamps ? stamps + (size_t)t * 4 * stamp_cap : nullptr, stamp_cap, wimg);
       if (rc != GNCA_OK) return rc;
       src = dst;
     }
@@ -2684,13 +2656,6 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
       if (hipStreamWaitEvent(sj[j], ss->fork, 0) != hipSuccess) return GNCA_ERR_HIP;
   }
   char* wsb = reinterpret_cast<char*>(ws);
-  if (dyn)
-    for (int j = 0; j < nsub; ++j) {
-      Plan Q;
-      if (!make_plan(&sd[j], false, &Q)) return GNCA_ERR_INVALID;
-      if (Q.var->split == 1 && hipMemsetAsync(wsb + off[j] + Q.off_tctr, 0, 16 * sizeof(int), sj[j]) != hipSuccess)
-        return GNCA_ERR_HIP;
-    }
   int rc = GNCA_OK;
   for (int t = 0; t < steps && rc == GNCA_OK; ++t) {
     const float* src = t == 0 ? x : (((steps - t) % 2 == 0) ? x_final : scratch);
@@ -2701,7 +2666,7 @@ static int rollout_impl(const gnca_step_desc* desc, const gnca_weights* w, int32
       rc = step_impl(&sd[j], w, src + elem0[j], dst + elem0[j], nullptr, nullptr, wsb + off[j], wsz[j], sj[j],
                      GNCA_PHASE_ALL, nullptr, hand_alive && (t > 0 || in0),
                      hand_alive && (t + 1 < steps || out_last), true,
-                     stamps ? stamps + ((size_t)t * nsub + j) * 4 * stamp_cap : nullptr, stamp_cap, wimg, 0, true, dyn);
+                     stamps ? stamps + ((size_t)t * nsub + j) * 4 * stamp_cap : nullptr, stamp_cap, wimg, 0, true);
     }
   }
   // join (also after a failed launch: the helper streams' work stays ordered before the caller's);

@@ -10,7 +10,7 @@ mkdir -p /tmp/k1probe
 cat > /tmp/k1probe/probe.hip <<EOT
 #define GNCA_K1_PROBE 1
 #include "$ROOT/graph_neural_cellular_automata_amd/csrc/gnca_step.hip"
-template __global__ void ${K:-gnca_k1_split_v192}<$ARGS>(const ${KA:-K1Args});
+template __global__ void ${K:-gnca_k1_split}<$ARGS>(const ${KA:-K1Args});
 }  // namespace gnca (left open by the GNCA_K1_PROBE cut)
 EOT
 cd /tmp/k1probe

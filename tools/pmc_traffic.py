@@ -32,6 +32,10 @@ res = {"fetch_correction": 2.0,
        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over "
                  "`python3 bench.py --steps 4 --warmup 1 --no-cpu` (tools/pmc.sh); "
                  "FETCH_SIZE x2 per tools/ubench/fetch_calib.hip",
+       # sha256[:16] of the libgnca.so the passes ran (set by the session script), so that a bench line
+       # can tell whether these counters belong to the build it timed
+       "lib_sha16": os.environ.get("GNCA_LIB_SHA16"),
+       "bench_args": os.environ.get("PMC_CMD") or os.environ.get("BENCH_ARGS"),
        "kernels": {}}
 for k, d in vals.items():
     m = {c: sum(v.values()) / len(v) for c, v in d.items()}
