@@ -1092,6 +1092,11 @@ __host__ __device__ inline int bc_stage(int TH, int TW, int RY, int RX, bool msg
 // One workgroup per (sample, tile); channels are pipelined through a double-buffered LDS
 // stage (the next channel's dY planes and dG halo are loaded into registers while this channel
 // is computed), one barrier per channel.
+// KC > 0: the offset count at compile time (the planned graph steps: 8, and 16 for C5): the
+// message adjoint's KC staged reads of a cell are issued together and its weights / source deltas
+// sit in registers, instead of a runtime loop that waited for each read in turn (same products in
+// the same order: the same bits).  KC = 0: any count.
+template <int KC>
 __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
@@ -1258,6 +1263,16 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
 #else
   const bool sobel = __syncthreads_and(pok) != 0;
 #endif
+  // KC > 0: the message adjoint's per-offset weights and staged-source deltas, in registers
+  float wk_[KC > 0 ? KC : 1];
+  int dk_[KC > 0 ? KC : 1];
+  if constexpr (KC > 0) {
+#pragma unroll
+    for (int o = 0; o < KC; ++o) {
+      wk_[o] = msg ? wts[o] : 0.f;
+      dk_[o] = a.offs[2 * o] * GW + (zp ? 0 : a.offs[2 * o + 1]);
+    }
+  }
   for (int c = c_lo; c < c_hi; ++c) {
     float* cur = ((c - c_lo) & 1) ? buf1 : buf0;
     float* nxt = ((c - c_lo) & 1) ? buf0 : buf1;
@@ -1306,9 +1321,17 @@ __global__ __launch_bounds__(kThreads) void gnca_b_adjoint(const BCArgs a) {
         // msg(p) = sum_o w_o A(p-o) M(p-o)  =>  gM(q) = A(q) sum_o w_o dm(q+o)  (roll / row shift)
         const float* g0 = cur + 3 * PA + (ti + RY) * GW + (tj + RX);
         float sg = 0.f;
-        for (int o = 0; o < k; ++o) {
-          const int dy = a.offs[2 * o], dx = zp ? 0 : a.offs[2 * o + 1];
-          sg = fmaf(wts[o], g0[dy * GW + dx], sg);
+        if constexpr (KC > 0) {
+          float gv[KC];
+#pragma unroll
+          for (int o = 0; o < KC; ++o) gv[o] = g0[dk_[o]];
+#pragma unroll
+          for (int o = 0; o < KC; ++o) sg = fmaf(wk_[o], gv[o], sg);
+        } else {
+          for (int o = 0; o < k; ++o) {
+            const int dy = a.offs[2 * o], dx = zp ? 0 : a.offs[2 * o + 1];
+            sg = fmaf(wts[o], g0[dy * GW + dx], sg);
+          }
         }
         acc = fmaf(as_[n], sg, acc);
       }
@@ -1555,50 +1578,60 @@ struct RedArgs {
   float* out[12];
 };
 
+// 32 columns per workgroup: a half-wave reads 32 consecutive floats of a partial row (one whole
+// 128-byte line; the 16-column form read 64-byte pieces of four rows per instruction), 336
+// workgroups for the 10,753 columns of the C = 16 step.  Each thread keeps the 16-column form's
+// arithmetic for two row groups rg = w + 8 v (rows rg + 16 i, four interleaved sums per group),
+// then the first 32 threads add the 16 groups in order: the same bits as before.
 __global__ __launch_bounds__(kThreads) void gnca_b_reduce(const RedArgs a) {
-  __shared__ double acc[16][17];
-  const int cj = threadIdx.x & 15, rg = threadIdx.x >> 4;
-  const int col = blockIdx.x * 16 + cj;
+  __shared__ double acc[16][33];
+  const int cj = threadIdx.x & 31, w = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + cj;
   int s = 0;
   while (s < a.nseg - 1 && col >= a.end[s]) ++s;
   const int begin = s == 0 ? 0 : a.end[s - 1];
   const long src = a.col0[s] + (long)(col - begin) * a.step[s];
-  double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+  const bool on = col < a.ncols && a.step[s] != 0;
   // U steps of 4 rows (rows r + 16 i, i < 4U): every load in flight before the adds, which keep the
   // one-step order (t0..t3 take rows r, r + 16, r + 32, r + 48 of each step), so the sums are the
   // same bits as one step at a time, in ceil(rows / 64U) memory latencies instead of rows / 64
   // (B=16 40^2: 960 rows, 15 dependent round trips per thread before)
-  auto steps = [&](auto U_, const auto* p, long& r) {
-    constexpr int U = decltype(U_)::value;
-    for (; r + 64 * (U - 1) + 48 < a.rows; r += 64 * U) {
-      double v[4 * U];
+#pragma unroll 1
+  for (int v = 0; v < 2; ++v) {
+    const int rg = w + 8 * v;
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+    auto steps = [&](auto U_, const auto* p, long& r) {
+      constexpr int U = decltype(U_)::value;
+      for (; r + 64 * (U - 1) + 48 < a.rows; r += 64 * U) {
+        double vv[4 * U];
 #pragma unroll
-      for (int i = 0; i < 4 * U; ++i) v[i] = (double)p[(r + 16 * i) * a.stride];
+        for (int i = 0; i < 4 * U; ++i) vv[i] = (double)p[(r + 16 * i) * a.stride];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        t0 += v[4 * u]; t1 += v[4 * u + 1]; t2 += v[4 * u + 2]; t3 += v[4 * u + 3];
+        for (int u = 0; u < U; ++u) {
+          t0 += vv[4 * u]; t1 += vv[4 * u + 1]; t2 += vv[4 * u + 2]; t3 += vv[4 * u + 3];
+        }
+      }
+    };
+    if (on) {
+      long r = rg;
+      if (a.f64) {
+        const double* p = reinterpret_cast<const double*>(a.part) + src;
+        steps(std::integral_constant<int, 8>{}, p, r);
+        steps(std::integral_constant<int, 2>{}, p, r);
+        steps(std::integral_constant<int, 1>{}, p, r);
+        for (; r < a.rows; r += 16) t0 += p[r * a.stride];
+      } else {
+        const float* p = reinterpret_cast<const float*>(a.part) + src;
+        steps(std::integral_constant<int, 8>{}, p, r);
+        steps(std::integral_constant<int, 2>{}, p, r);
+        steps(std::integral_constant<int, 1>{}, p, r);
+        for (; r < a.rows; r += 16) t0 += (double)p[r * a.stride];
       }
     }
-  };
-  if (col < a.ncols && a.step[s] != 0) {
-    long r = rg;
-    if (a.f64) {
-      const double* p = reinterpret_cast<const double*>(a.part) + src;
-      steps(std::integral_constant<int, 8>{}, p, r);
-      steps(std::integral_constant<int, 2>{}, p, r);
-      steps(std::integral_constant<int, 1>{}, p, r);
-      for (; r < a.rows; r += 16) t0 += p[r * a.stride];
-    } else {
-      const float* p = reinterpret_cast<const float*>(a.part) + src;
-      steps(std::integral_constant<int, 8>{}, p, r);
-      steps(std::integral_constant<int, 2>{}, p, r);
-      steps(std::integral_constant<int, 1>{}, p, r);
-      for (; r < a.rows; r += 16) t0 += (double)p[r * a.stride];
-    }
+    acc[rg][cj] = (t0 + t1) + (t2 + t3);
   }
-  acc[rg][cj] = (t0 + t1) + (t2 + t3);
   __syncthreads();
-  if (rg == 0 && col < a.ncols && a.out[s]) {
+  if (w == 0 && col < a.ncols && a.out[s]) {
     double v = 0.0;
     for (int g = 0; g < 16; ++g) v += acc[g][cj];
     a.out[s][col - begin] = (float)v;
@@ -1853,7 +1886,7 @@ struct Reducer {
   }
   int launch(hipStream_t st) {
     if (a.nseg == 0 || a.ncols == 0) return GNCA_OK;
-    hipLaunchKernelGGL(gnca_b_reduce, dim3((a.ncols + 15) / 16), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(gnca_b_reduce, dim3((a.ncols + 31) / 32), dim3(kThreads), 0, st, a);
     return bwd_check();
   }
 };
@@ -2093,7 +2126,8 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
     a.uniform_w = P.F.k > 0 ? (float)(1.0 / (double)P.F.k) : 0.f;
     a.flags = (d.flags & (GNCA_ZERO_PAD_SHIFT | GNCA_ALIVE_TO_ALIVE)) | (P.msg ? kMsg : 0u);
     for (int o = 0; o < 2 * a.k; ++o) a.offs[o] = d.offsets[o];
-    hipLaunchKernelGGL(gnca_b_adjoint, dim3(B * P.tps3 * a.ncg), dim3(kThreads), P.ldsC, st, a);
+    hipLaunchKernelGGL(a.k == 8 ? gnca_b_adjoint<8> : a.k == 16 ? gnca_b_adjoint<16> : gnca_b_adjoint<0>,
+                       dim3(B * P.tps3 * a.ncg), dim3(kThreads), P.ldsC, st, a);
     if ((rc = bwd_check()) != GNCA_OK) return rc;
   }
   if (!P.graph || !(P.msg && P.zp)) return GNCA_OK;
