@@ -1674,6 +1674,9 @@ static const Variant kVariants[] = {
     GNCA_SV(36, 24, 4, 4, 8),
     GNCA_SV(24, 24, 4, 4, 8),
     GNCA_SVF(8, 24, 4, 4, 8, reinterpret_cast<const void*>(&gnca_k1_split<8, 24, 4, 4, 8, 1>)),
+    // classic NCA steps (and the graph model's message-off steps: the trainers' message_every) at
+    // large batches: 24x36 tiles (round 6; before, the 8x24 small-batch tiles served every batch)
+    GNCA_SVF(24, 36, 1, 4, 0, nullptr),   // + the compact fold (on request)
     GNCA_SVF(8, 24, 1, 4, 0, reinterpret_cast<const void*>(&gnca_k1_split<8, 24, 1, 4, 0, 1>)),   // classic NCA
                                  // (no gather; RX 4 keeps the staging rows quad-aligned)
     GNCA_SV(8, 20, 4, 4, 8),
@@ -1889,8 +1892,8 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
   // the compact field (each field + 256 B: the finalizer's quad reads may touch one float past it)
   // (the update field is compact for large batches and dense NCHW for small ones)
   // (the preparer sums a sample's partials in one wave pass: tps * waves <= 256)
-  // The fold on the compact field (large batches) is built and bitwise-tested but not planned by
-  // default: measured on the headline (B=1024 72^2) it runs 0.566 ms/step against 0.504 for the
+  // The fold on the compact field (large batches) is not planned where the sub-batch pipeline runs:
+  // measured on the headline (B=1024 72^2) it runs 0.566 ms/step against 0.504 for the
   // sub-batch pipeline (K1 + K2 on two streams), because the finalize of each tile's 1.63x halo
   // region comes after the tile's groups and waits on its loads ("The fold").  Small
   // batches (dense field) fold: one launch per step instead of two (BASELINE c2 18.6 -> 15.7 us,
@@ -1903,10 +1906,17 @@ static bool make_plan(const gnca_step_desc* d, bool msg_only, Plan* P) {
 #ifdef GNCA_NO_FOLD   // A/B builds: no fold at all
   P->fold_any = false;
 #endif
+  // Round 6: the compact fold is the default too where a rollout runs ONE stream on the compact field
+  // (a batch whose halves are below the compact field's threshold, so no sub-batch pipeline: C4's
+  // 128-sample shard): there the separate K2 is not hidden beside another K1, and one K1 launch per
+  // step wins (B=128 72^2: 0.0779 vs 0.0819 ms/step; B=256, two streams: 0.150 vs 0.126 without,
+  // profiles/r06f_b128_ab.txt)
+  const bool one_stream = P->compact_ok && P->var->TH > 0 &&
+                          (long)(d->B / 2) * P->tps < 2L * device_cus() * std::max(1, 512 / P->var->NT);
 #ifdef GNCA_FOLD_COMPACT_DEFAULT   // A/B builds: the compact fold planned by default too
   P->fold_ok = P->fold_any;
 #else
-  P->fold_ok = P->fold_any && !P->compact_ok;
+  P->fold_ok = P->fold_any && (!P->compact_ok || one_stream);
 #endif
   const bool fc = P->fold_any && P->compact_ok;
   P->off_dx2 = carve(P->fold_any ? n * 4 + 256 : 0);

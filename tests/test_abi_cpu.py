@@ -144,6 +144,12 @@ def test_k1_variant_names(lib):
     assert name(1024, 16, 72, r4) == ("gnca_k1_split<24,36,4,4,8>", "bf16x6")
     assert name(8, 16, 72, r4) == ("gnca_k1_split<8,24,4,4,8>", "bf16x6")
     assert name(8, 16, 72, [], graph=False) == ("gnca_k1_split<8,24,1,4,0>", "bf16x6")
+    # classic steps at large batches (and the trainers' message-off graph steps): 24x36 tiles
+    assert name(128, 16, 72, [], graph=False) == ("gnca_k1_split<24,36,1,4,0>", "bf16x6")
+    d_off = S.make_desc(B=128, C=16, H=72, W=72, hidden=128, d_model=16, offsets=r4, flags=flags,
+                        update_gain=0.05, alpha_thr=0.12, message_gain=0.0, fire_rate=0.5,
+                        fire_mode=L_.FIRE_HASH)
+    assert S.k1_variant(d_off) == ("gnca_k1_split<24,36,1,4,0>", "bf16x6")
     assert name(128, 32, 128, r5) == ("gnca_k1_split32<16,16,5,8,16>", "bf16x6")
     # the rollout's compact update field: large batches on the bf16-split K1s only
     comp = lambda B, C, H, offs, graph=True: S.rollout_compact(S.make_desc(

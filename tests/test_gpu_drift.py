@@ -27,9 +27,13 @@ CASES = {
     # the headline's shape class: B=96 x 16 x 72^2 graph torus r=4 K=8 -> 576 tiles of 24x36
     "graph_split24x36": ("graph_torus_latest_grown_b1_72", True, 16, 72, 96, 4, 8, 96, (0, 47, 95),
                          "gnca_k1_split<24,36,4,4,8>", True),
-    # classic NCA (BASELINE config 2's step) on the classic split K1
-    "classic_split8x24": ("classic_ep980_b2_32", False, 16, 72, 96, 0, 0, 96, (0, 47, 95),
-                          "gnca_k1_split<8,24,1,4,0>", True),
+    # classic NCA at a large batch (and the trainers' message-off graph steps): the 24x36 classic
+    # split K1 (round 6), compact field, sub-batch pipeline
+    "classic_split24x36": ("classic_ep980_b2_32", False, 16, 72, 96, 0, 0, 96, (0, 47, 95),
+                           "gnca_k1_split<24,36,1,4,0>", True),
+    # BASELINE config 2's shape (classic, B=8): the small-tile classic split K1, dense fold
+    "classic_split8x24": ("classic_ep980_b2_32", False, 16, 72, 8, 0, 0, 96, (0, 7),
+                          "gnca_k1_split<8,24,1,4,0>", False),
     # BASELINE config 3 (graph torus r=4 K=8, B=8, 72^2): the small-batch split K1 on 8x24 tiles,
     # dense update field
     "c3_split8x24": ("graph_torus_latest_grown_b1_72", True, 16, 72, 8, 4, 8, 96, (0, 7),

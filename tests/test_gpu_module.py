@@ -214,7 +214,9 @@ def test_compact_rollout_equals_dense_steps(dev, graph):
 
     name, arith = S.k1_variant(desc(0))
     assert arith == "bf16x6", name
-    assert not S.rollout_fold(desc(0)) and S.rollout_fold(desc(0), possible=True)
+    # B=128: one stream on the compact field (its halves are below the sub-batch threshold), which
+    # folds by default since round 6
+    assert S.rollout_subs(desc(0)) == 1 and S.rollout_fold(desc(0)) and S.rollout_fold(desc(0), possible=True)
     r = S.rollout(desc(0), w, x.contiguous(), steps, offs)
     # the fold on request (each finish inside the next K1, the compact field double-buffered)
     assert torch.equal(S.rollout(desc(0), w, x.contiguous(), steps, offs, fold=True), r)
@@ -541,8 +543,10 @@ def test_fold_rollout_pieces_bitwise(dev, B, graph):
 
     compact = B > 8
     assert S.rollout_compact(desc(0)) == compact
-    # small batches fold by default; the compact field folds on request (GNCA_ROLLOUT_FOLD)
-    assert S.rollout_fold(desc(0)) == (not compact) and S.rollout_fold(desc(0), possible=True)
+    # small batches fold by default, and so does the compact field where the rollout runs one stream
+    # (B=160: its halves are below the sub-batch threshold); otherwise it folds on request
+    default_fold = (not compact) or S.rollout_subs(desc(0)) == 1
+    assert S.rollout_fold(desc(0)) == default_fold and S.rollout_fold(desc(0), possible=True)
     one = S.rollout(desc(0), w, x.contiguous(), steps, offs, fold=True)
     cur = x
     for t in range(steps):
@@ -575,8 +579,8 @@ def test_fold_rollout_pieces_bitwise(dev, B, graph):
     if not (graph and B > 8):
         return
     arr = (ctypes.c_int8 * 16)(*[v for p in offs[0] for v in p])
-    for fl in (L.ROLLOUT_PENDING_OUT | L.ROLLOUT_ALIVE_OUT, L.ROLLOUT_PENDING_IN | L.ROLLOUT_ALIVE_IN,
-               L.ROLLOUT_PENDING_OUT):   # (the last: no fold without GNCA_ROLLOUT_FOLD on the compact field)
+    for fl in (L.ROLLOUT_PENDING_OUT | L.ROLLOUT_ALIVE_OUT, L.ROLLOUT_PENDING_IN | L.ROLLOUT_ALIVE_IN) + \
+            (() if default_fold else (L.ROLLOUT_PENDING_OUT,)):   # (no fold without GNCA_ROLLOUT_FOLD there)
         assert lib.gnca_rollout_ex_f32(ctypes.byref(desc(0)), ctypes.byref(w), 1, arr, x.data_ptr(),
                                        scratch.data_ptr(), torch.empty_like(x).data_ptr(), ws.data_ptr(),
                                        ws.numel(), fl, st) == -1
