@@ -1769,8 +1769,10 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
 #ifndef GNCA_BB_NO_SPEC   // A/B builds: no compile-time-geometry instance
   if (C == 16 && P->CP == 16 && P->bb->HB == 128 && Hd == 128)
     for (const BBSpec& sp : kBBS)
-      if (sp.TH == P->TH && sp.TW == P->TW && sp.RY == P->RY && sp.RX == rxb && sp.K == P->F.k &&
-          (P->msg ? sp.K > 0 : sp.K == 0))
+      // (a graph step without the message, e.g. the trainers' message-off steps, is a classic step
+      //  for BB whatever offsets were drawn: the K = 0 instance; round 6, before it took the
+      //  runtime-geometry kernel)
+      if (sp.TH == P->TH && sp.TW == P->TW && sp.RY == P->RY && sp.RX == rxb && sp.K == (P->msg ? P->F.k : 0))
         P->bbfn = P->bbfn2 = sp.fn;
 #endif
 #endif
