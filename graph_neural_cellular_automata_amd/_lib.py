@@ -73,7 +73,7 @@ EXPORTS = ("gnca_abi_version", "gnca_status_string", "gnca_last_hip_error",
            "gnca_perceive_f32", "gnca_rollout_f32", "gnca_bwd_workspace_bytes", "gnca_step_bwd_f32",
            "gnca_fire_mask_u8", "gnca_step_masked_f32", "gnca_damage_f32", "gnca_loss_premult_f32",
            "gnca_loss_premult_bwd_f32", "gnca_k1_variant", "gnca_rollout_stamped_f32",
-           "gnca_rollout_ex_f32")
+           "gnca_rollout_ex_f32", "gnca_bb_variant")
 
 PHASE_K0, PHASE_K1, PHASE_K2 = 1, 2, 4
 PHASE_ALL = 7
@@ -144,6 +144,8 @@ def load(path: str = LIB_PATH):
     lib.gnca_damage_f32.argtypes = [ctypes.POINTER(DamageDesc), vp, vp, vp, vp]
     lib.gnca_k1_variant.restype = ctypes.c_int
     lib.gnca_k1_variant.argtypes = [ctypes.POINTER(StepDesc), ctypes.c_char_p, i32, ctypes.POINTER(ctypes.c_int32)]
+    lib.gnca_bb_variant.restype = ctypes.c_int
+    lib.gnca_bb_variant.argtypes = [ctypes.POINTER(StepDesc), ctypes.c_char_p, i32]
     lib.gnca_step_masked_f32.restype = ctypes.c_int
     lib.gnca_step_masked_f32.argtypes = [ctypes.POINTER(StepDesc), ctypes.POINTER(Weights), vp, vp, vp,
                                          vp, vp, sz, vp]

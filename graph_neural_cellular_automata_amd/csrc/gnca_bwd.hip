@@ -318,7 +318,11 @@ struct BBLayout {
   int ST1, ST2, ST3, SCRW, RH, RW, NI, NIA, total;
 };
 
-__host__ __device__ inline BBLayout bb_layout(int CP, int HB, int TH, int TW, int RY, int RX, int kmax) {
+// lean (the large-tile instances, LL below): no W1^T image (dY's A fragments are read from the W1
+// image, one float each) and the per-wave dh / h transposes staged half a slice at a time, so that a
+// 24x24 tile's 32x32 staged region fits 160 KB
+__host__ __device__ inline BBLayout bb_layout(int CP, int HB, int TH, int TW, int RY, int RX, int kmax,
+                                              bool lean = false) {
   BBLayout L;
   L.RH = TH + 2 * RY;
   L.RW = TW + 2 * RX;
@@ -332,7 +336,7 @@ __host__ __device__ inline BBLayout bb_layout(int CP, int HB, int TH, int TW, in
   L.S1T = odd4(4 * MT);
   L.S2T = odd4(4 * MO);
   L.SWM = odd4(CPM);
-  L.ST1 = s16(HB);
+  L.ST1 = s16(lean ? HB / 2 : HB);
   L.ST2 = s16(3 * CP);
   L.ST3 = s16(CP);
   L.SCRW = 16 * (L.ST1 + std::max(L.ST2, 2 * L.ST3));   // T3/T4 reuse T2's rows (after dW1)
@@ -343,7 +347,7 @@ __host__ __device__ inline BBLayout bb_layout(int CP, int HB, int TH, int TW, in
   L.kp = o; o += r4(TH * TW);
   L.lst = o; o += r4(TH * TW) + 8;   // compacted live-cell list + per-wave counts
   L.w1f = o; o += MT * 64 * L.KSP;   // W1 fragments (GEMM1 recompute)
-  L.w1t = o; o += FT * 64 * L.S1T;   // W1^T fragments (dY = W1^T dh)
+  L.w1t = o; o += lean ? 0 : FT * 64 * L.S1T;   // W1^T fragments (dY = W1^T dh)
   L.w2t = o; o += MT * 64 * L.S2T;   // W2^T fragments (dh = W2^T d_pre)
   L.wms = o; o += CPM * L.SWM;
   L.b1s = o; o += r4(HB);
@@ -391,12 +395,15 @@ struct BBArgs {
 // runtime C those tests were 64-bit lane masks held across the group loop (SGPR spills)
 // TH_ .. K_ (all > 0, K_ >= 0): the tile geometry and offset count at compile time (the planned
 // shapes of the C = 16 graph and classic steps, kBBS below): every LDS offset and loop bound a constant
-template <int CP, int HB, bool FULL = false, int TH_ = 0, int TW_ = 0, int RY_ = 0, int RX_ = 0, int K_ = -1>
+// LL: the lean LDS layout (bb_layout's `lean`) of the large-tile instances
+template <int CP, int HB, bool FULL = false, int TH_ = 0, int TW_ = 0, int RY_ = 0, int RX_ = 0, int K_ = -1,
+          bool LL = false>
 __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CPQ = CP / 4, KS = 3 * CPQ, MT = HB / 16, MO = (CP + 15) / 16, FT = (3 * CP + 15) / 16;
   const int TH = TH_ ? TH_ : a.TH, TW = TW_ ? TW_ : a.TW, RY = RY_ ? RY_ : a.RY, RX = RX_ ? RX_ : a.RX;
-  const BBLayout L = bb_layout(CP, HB, TH, TW, RY, RX, K_ >= 0 ? K_ : a.k);
+  static_assert(!LL || (HB / 16) % 2 == 0, "lean layout: two halves of whole 16-unit tiles");
+  const BBLayout L = bb_layout(CP, HB, TH, TW, RY, RX, K_ >= 0 ? K_ : a.k, LL);
   const int RH = L.RH, RW = L.RW, PSTR = L.PSTR, ALW = L.ALW;
   const int KSP = L.KSP, S1T = L.S1T, S2T = L.S2T, SWM = L.SWM, ST1 = L.ST1, ST2 = L.ST2, ST3 = L.ST3;
   float* xs = smem + L.xs;
@@ -452,7 +459,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       const int s = idx % cKSP, ml = idx / cKSP, l = ml & 63, m = ml >> 6;
       return s < KS ? w1at(h0 + 16 * m + (l & 15), 4 * s + (l >> 4)) : 0.f;
     });
-    f2.load(tid, [&](int idx) {   // A[slot][hid], k-step (m, r)
+    if constexpr (!LL) f2.load(tid, [&](int idx) {   // A[slot][hid], k-step (m, r)
       const int e = idx % cS1T, fl = idx / cS1T, l = fl & 63, ft = fl >> 6;
       const int m = e >> 2, r = e & 3;
       return e < 4 * MT ? w1at(h0 + 16 * m + 4 * (l >> 4) + r, 16 * ft + (l & 15)) : 0.f;
@@ -474,7 +481,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       return (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
     });
     f1.store(w1f, tid);
-    f2.store(w1t, tid);
+    if constexpr (!LL) f2.store(w1t, tid);
     f3.store(w2t, tid);
     f4_.store(wms, tid);
     f5.store(b1s, tid);
@@ -872,8 +879,18 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           f4 wv[FT];
+          if constexpr (LL) {
+            // A[slot = 16ft + c16][hid = 16m + 4g + r] from the W1 image: W1[16m + (l & 15)][4s + (l >> 4)]
+            // sits at w1f[(64m + l) KSP + s], here l = 4g + r + 16 (c16 & 3), s = 4ft + (c16 >> 2)
+            const float* wl = w1f + (4 * g + 16 * (c16 & 3)) * KSP + (c16 >> 2) + m * 64 * KSP;
 #pragma unroll
-          for (int ft = 0; ft < FT; ++ft) wv[ft] = *reinterpret_cast<const f4*>(w1t + (ft * 64 + lane) * S1T + 4 * m);
+            for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) wv[ft][r] = wl[r * KSP + 4 * ft];
+          } else {
+#pragma unroll
+            for (int ft = 0; ft < FT; ++ft) wv[ft] = *reinterpret_cast<const f4*>(w1t + (ft * 64 + lane) * S1T + 4 * m);
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -949,38 +966,48 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       }
       __builtin_amdgcn_sched_barrier(0);
       // -- weight gradients, the cell dimension as the MFMA K (per-wave LDS transposes) --
-#pragma unroll
-      for (int m = 0; m < MT; ++m) *reinterpret_cast<f4*>(T1 + c16 * ST1 + 16 * m + 4 * g) = dh[m];
+      // (LL: T1 holds half the slice's hidden units at a time; every accumulator sums its k-steps in
+      //  the same order either way)
+      constexpr int NHH = LL ? 2 : 1, MH = MT / NHH;
 #pragma unroll
       for (int s = 0; s < KS; ++s) T2[c16 * ST2 + 4 * s + g] = y[s];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int row = 4 * s4 + g;
-        float bv[FT];
+      for (int hh = 0; hh < NHH; ++hh) {
 #pragma unroll
-        for (int ft = 0; ft < FT; ++ft) bv[ft] = T2[row * ST2 + 16 * ft + c16];
+        for (int m = 0; m < MH; ++m) *reinterpret_cast<f4*>(T1 + c16 * ST1 + 16 * m + 4 * g) = dh[MH * hh + m];
 #pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          const float av = T1[row * ST1 + 16 * m + c16];
-          ab1[m] += av;
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int row = 4 * s4 + g;
+          float bv[FT];
 #pragma unroll
-          for (int ft = 0; ft < FT; ++ft)
-            aw1[m][ft] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[ft], aw1[m][ft], 0, 0, 0);
+          for (int ft = 0; ft < FT; ++ft) bv[ft] = T2[row * ST2 + 16 * ft + c16];
+#pragma unroll
+          for (int m = 0; m < MH; ++m) {
+            const float av = T1[row * ST1 + 16 * m + c16];
+            ab1[MH * hh + m] += av;
+#pragma unroll
+            for (int ft = 0; ft < FT; ++ft)
+              aw1[MH * hh + m][ft] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[ft], aw1[MH * hh + m][ft], 0, 0, 0);
+          }
         }
       }
 #pragma unroll
-      for (int m = 0; m < MT; ++m) *reinterpret_cast<f4*>(T1 + c16 * ST1 + 16 * m + 4 * g) = hp[m];
-#pragma unroll
       for (int mo = 0; mo < MO; ++mo) *reinterpret_cast<f4*>(T3 + c16 * ST3 + 16 * mo + 4 * g) = dp[mo];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int row = 4 * s4 + g;
+      for (int hh = 0; hh < NHH; ++hh) {
 #pragma unroll
-        for (int mo = 0; mo < MO; ++mo) {
-          const float av = T3[row * ST3 + 16 * mo + c16];
+        for (int m = 0; m < MH; ++m) *reinterpret_cast<f4*>(T1 + c16 * ST1 + 16 * m + 4 * g) = hp[MH * hh + m];
 #pragma unroll
-          for (int m = 0; m < MT; ++m)
-            aw2[mo][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, T1[row * ST1 + 16 * m + c16], aw2[mo][m], 0, 0, 0);
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int row = 4 * s4 + g;
+#pragma unroll
+          for (int mo = 0; mo < MO; ++mo) {
+            const float av = T3[row * ST3 + 16 * mo + c16];
+#pragma unroll
+            for (int m = 0; m < MH; ++m)
+              aw2[mo][MH * hh + m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, T1[row * ST1 + 16 * m + c16],
+                                                                         aw2[mo][MH * hh + m], 0, 0, 0);
+          }
         }
       }
       if (msg_bwd) {
@@ -1656,15 +1683,19 @@ static const BBVariant kBB[] = {
 };
 #undef GNCA_BV
 // compile-time-geometry instances of the planned shapes (16 channels, hidden 128, x halo padded to 4):
-// 72^2 canvases take 8x24 tiles, the trainer's 40^2 8x16; graph r <= 4 (the y halo padded to 4) with
-// 8 offsets, or classic (y halo 1, no offsets)
+// 72^2 canvases take 8x24 tiles (24x24 in the lean layout when the batch fills the chip), the
+// trainer's 40^2 8x16; graph r <= 4 (the y halo padded to 4) with 8 offsets, or classic (y halo 1, no
+// offsets)
 struct BBSpec {
   int TH, TW, RY, RX, K;
+  bool lean;
   const void* fn;
 };
-#define GNCA_BS(th, tw, ry, rx, k) {th, tw, ry, rx, k, reinterpret_cast<const void*>(&gnca_b_mlp<16, 128, true, th, tw, ry, rx, k>)}
+#define GNCA_BS(th, tw, ry, rx, k, ll) \
+  {th, tw, ry, rx, k, ll, reinterpret_cast<const void*>(&gnca_b_mlp<16, 128, true, th, tw, ry, rx, k, ll>)}
 static const BBSpec kBBS[] = {
-    GNCA_BS(8, 24, 4, 4, 8), GNCA_BS(8, 16, 4, 4, 8), GNCA_BS(8, 24, 1, 4, 0), GNCA_BS(8, 16, 1, 4, 0),
+    GNCA_BS(8, 24, 4, 4, 8, false), GNCA_BS(8, 16, 4, 4, 8, false), GNCA_BS(8, 24, 1, 4, 0, false),
+    GNCA_BS(8, 16, 1, 4, 0, false), GNCA_BS(24, 24, 4, 4, 8, true), GNCA_BS(24, 24, 1, 4, 0, true),
 };
 #undef GNCA_BS
 
@@ -1674,6 +1705,7 @@ struct BwdPlan {
   const void* bbfn;    // the BB kernel: bb->fn
   const void* bbfn2;   // the kernel of slices after the first (bb->fn)
   bool bbf32;          // BB is gnca_b_mlp (keep bytes, 16-byte staging): always, since round 6
+  bool bblean;         // BB runs a lean-layout compile-time instance (kBBS, large tiles)
   int CP, HB, nslices;
   bool graph, msg, zp, gn;
   int RY, RX;
@@ -1704,7 +1736,10 @@ static int bwd_device_cus() {
   return cus;
 }
 
-static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
+// lean_ok: the large lean-layout tiles may be planned.  Not for a masked step (an active-sample mask):
+// its late steps have few active samples, whose work 3x larger tiles spread over fewer CUs (the B=128
+// trainer iteration measured 111-113 -> 116-120 ms with them, profiles/r06g_bb_lean_ab.txt)
+static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P, bool lean_ok = true) {
   if (!d || !fwd_layout(d, &P->F)) return false;
   const int C = d->C, Hd = d->hidden, H = d->H, W = d->W;
   P->CP = (C + 3) & ~3;
@@ -1736,15 +1771,37 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
   if (tile_env) sscanf(tile_env, "%dx%d", &eth, &etw);
   double best = 1e300;
   P->bb = nullptr;
+  P->bblean = false;
+  // the compile-time instance this step's shape would run on a (th, tw) tile, if any
+  const bool spec_ok = C == 16 && P->CP == 16 && Hd == 128;
+  auto spec_for = [&](int th, int tw) -> const BBSpec* {
+    if (!spec_ok) return nullptr;
+    for (const BBSpec& sp : kBBS)
+      // (a graph step without the message, e.g. the trainers' message-off steps, is a classic step
+      //  for BB whatever offsets were drawn: the K = 0 instance; round 6, before it took the
+      //  runtime-geometry kernel)
+      if (sp.TH == th && sp.TW == tw && sp.RY == ry && sp.RX == rxb && sp.K == (P->msg ? P->F.k : 0)) return &sp;
+    return nullptr;
+  };
+  static const int ths_lean[] = {24};
   for (const BBVariant& v : kBB) {
     if (v.CP != P->CP) continue;
     const int ns = (Hd + v.HB - 1) / v.HB;
     const int padh = ns * v.HB - Hd;
-    for (int th : ths)
+    for (int pass = 0; pass < 2; ++pass)
+    for (int thi = 0; thi < (pass ? 1 : 3); ++thi)
       for (int tw : tws) {
+        const int th = pass ? ths_lean[thi] : ths[thi];
+        if (pass && v.HB != 128) continue;
         if ((th * tw) % 64 || tw + 2 * rxb + 2 > 64) continue;   // staging rows fit one wave
         if (eth && (th != eth || tw != etw)) continue;
-        const BBLayout L = bb_layout(P->CP, v.HB, th, tw, ry, rxb, P->F.k);
+        // (pass 1: the large tiles, only in the lean layout of a compile-time instance)
+        const BBSpec* lsp = pass ? spec_for(th, tw) : nullptr;
+        if (pass && !(lean_ok && lsp && lsp->lean)) continue;
+#if defined(GNCA_BB_NO_LEAN) || defined(GNCA_BB_NO_SPEC) || defined(GNCA_BB_NO_FULL)
+        if (pass) continue;   // A/B builds: the plans of round 6 (8x24 at 72^2) / no compile-time instance
+#endif
+        const BBLayout L = bb_layout(P->CP, v.HB, th, tw, ry, rxb, P->F.k, pass == 1);
         const size_t bytes = (size_t)L.total * 4;
         if (bytes > 160 * 1024) continue;
         const long tx = (W + tw - 1) / tw, ty = (H + th - 1) / th;
@@ -1757,7 +1814,7 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
         const double tcost = (double)std::max<long>(rounds * cus, tiles) * per_tile;
         const double cost = 1e12 * ns + 1e9 * padh + tcost;
         if (cost < best) {
-          best = cost; P->bb = &v; P->TH = th; P->TW = tw; P->ldsB = bytes;
+          best = cost; P->bb = &v; P->TH = th; P->TW = tw; P->ldsB = bytes; P->bblean = pass == 1;
         }
       }
   }
@@ -1767,15 +1824,14 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P) {
 #else
   P->bbfn = P->bbfn2 = (C == P->CP && P->bb->fnf) ? P->bb->fnf : P->bb->fn;
 #ifndef GNCA_BB_NO_SPEC   // A/B builds: no compile-time-geometry instance
-  if (C == 16 && P->CP == 16 && P->bb->HB == 128 && Hd == 128)
-    for (const BBSpec& sp : kBBS)
-      // (a graph step without the message, e.g. the trainers' message-off steps, is a classic step
-      //  for BB whatever offsets were drawn: the K = 0 instance; round 6, before it took the
-      //  runtime-geometry kernel)
-      if (sp.TH == P->TH && sp.TW == P->TW && sp.RY == P->RY && sp.RX == rxb && sp.K == (P->msg ? P->F.k : 0))
-        P->bbfn = P->bbfn2 = sp.fn;
+  if (P->bb->HB == 128)
+    if (const BBSpec* sp = spec_for(P->TH, P->TW))
+      if (sp->lean == P->bblean) P->bbfn = P->bbfn2 = sp->fn;
 #endif
 #endif
+  // a lean-layout plan runs only on its compile-time instance (the runtime-geometry kernels use the
+  // full layout)
+  if (P->bblean && (P->bbfn != spec_for(P->TH, P->TW)->fn)) return false;
   P->bbf32 = true;
   P->RXB = rxb;
   // (a split-arithmetic BB on bf16 MFMA was built and measured slower, 4.09 vs 3.24 ms for BB at
@@ -1966,9 +2022,21 @@ int gnca_bprof_dump(unsigned long long* out) {
 #endif
 
 size_t gnca_bwd_workspace_bytes(const gnca_step_desc* desc) {
+  BwdPlan P, Q;   // enough for the full-batch plan and the masked step's
+  if (!bwd_plan(desc, &P) || !bwd_plan(desc, &Q, false)) return 0;
+  return std::max(P.bytes, Q.bytes);
+}
+
+int gnca_bb_variant(const gnca_step_desc* desc, char* name, int32_t n) {
   BwdPlan P;
-  if (!bwd_plan(desc, &P)) return 0;
-  return P.bytes;
+  if (!name || n <= 0 || !bwd_plan(desc, &P)) return GNCA_ERR_INVALID;
+  int th = 0, tw = 0, ry = 0, rx = 0, k = -1;
+  bool full = P.bbfn == P.bb->fnf && P.bb->fnf != nullptr, lean = false;
+  for (const BBSpec& sp : kBBS)
+    if (sp.fn == P.bbfn) { th = sp.TH; tw = sp.TW; ry = sp.RY; rx = sp.RX; k = sp.K; lean = sp.lean; full = true; }
+  snprintf(name, (size_t)n, "gnca_b_mlp<%d,%d,%d,%d,%d,%d,%d,%d,%d>", P.CP, P.HB, full ? 1 : 0, th, tw, ry, rx, k,
+           lean ? 1 : 0);
+  return GNCA_OK;
 }
 
 int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const float* x,
@@ -1982,7 +2050,7 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
   gnca_step_desc d = *desc;
   d.flags &= ~GNCA_ATTENTION;
   BwdPlan P;
-  if (!bwd_plan(&d, &P)) return GNCA_ERR_INVALID;
+  if (!bwd_plan(&d, &P, active == nullptr)) return GNCA_ERR_INVALID;
   if (!ws || ws_bytes < P.bytes) return GNCA_ERR_WORKSPACE;
   if (P.gn && (!w->gn_weight || !w->gn_bias)) return GNCA_ERR_INVALID;
   if (P.msg && (!w->wm || !w->bm)) return GNCA_ERR_INVALID;

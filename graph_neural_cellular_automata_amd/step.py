@@ -140,6 +140,14 @@ def k1_variant(desc: L.StepDesc) -> tuple[str, str]:
     return buf.value.decode(), ("bf16x6" if arith.value & 1 else "f32")
 
 
+def bb_variant(desc: L.StepDesc) -> str:
+    """The backward MLP kernel (BB) the backward plan for ``desc`` launches, as
+    "gnca_b_mlp<CP,HB,FULL,TH,TW,RY,RX,K,LEAN>" (gnca_bb_variant, host-only)."""
+    buf = ctypes.create_string_buffer(128)
+    L.check(L.load().gnca_bb_variant(ctypes.byref(desc), buf, 128), "gnca_bb_variant")
+    return buf.value.decode()
+
+
 def rollout_compact(desc: L.StepDesc) -> bool:
     """True when a rollout of ``desc``'s shape runs on the compact update field (K1 packs the live
     cells' dx per tile, K2 unpacks them: GNCA_PHASE_COMPACT)."""

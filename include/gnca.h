@@ -286,6 +286,12 @@ typedef struct gnca_grads {
 /* Bytes of device workspace gnca_step_bwd_f32 needs for `desc` (0 on invalid desc). */
 size_t gnca_bwd_workspace_bytes(const gnca_step_desc* desc);
 
+/* Measurement: the backward MLP kernel (BB) the plan for `desc` launches without an active-sample
+ * mask, as "gnca_b_mlp<CP,HB,FULL,TH,TW,RY,RX,K,LEAN>" (TH .. K 0 / -1 for the runtime-geometry
+ * kernels; NUL-terminated, truncated to n bytes); a masked step never takes the LEAN (24x24) tiles.
+ * Host-only.  Returns GNCA_OK or GNCA_ERR_INVALID. */
+int gnca_bb_variant(const gnca_step_desc* desc, char* name, int32_t n);
+
 /*
  * Vector-Jacobian product of one step: given the step input x (and the same desc, weights and
  * fire input as the forward call) and gy = dL/d x_out, write gx = dL/dx and the parameter

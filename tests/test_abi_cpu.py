@@ -162,3 +162,32 @@ def test_k1_variant_names(lib):
     assert nm.startswith("gnca_k1_update<12,64,") and ar == "f32"
     buf = ctypes.create_string_buffer(8)
     assert lib.gnca_k1_variant(None, buf, 8, None) != 0
+
+
+def test_bb_variant_names(lib):
+    """gnca_bb_variant (host-only) names the backward MLP kernel each training shape plans: the
+    lean-layout 24x24 instances once a 72^2 batch fills the chip (B >= 96), 8x24 below (B >= 8), the
+    graph (K = 8) and the classic / message-off (K = 0) instances, the runtime-geometry kernel
+    elsewhere."""
+    from graph_neural_cellular_automata_amd import _lib as L_
+    flags = L_.USE_GROUPNORM | L_.GRAPH | L_.HIDDEN_ONLY | L_.ALIVE_TO_ALIVE
+    r4 = [(dy, dx) for dy in range(-4, 5) for dx in range(-4, 5) if max(abs(dy), abs(dx)) > 1][:8]
+
+    def name(B, H, offs, graph=True, gain=0.25, C=16):
+        d = S.make_desc(B=B, C=C, H=H, W=H, hidden=128, d_model=16, offsets=offs,
+                        flags=flags if graph else L_.USE_GROUPNORM, update_gain=0.05, alpha_thr=0.12,
+                        message_gain=gain, fire_rate=0.5, fire_mode=L_.FIRE_HASH)
+        return S.bb_variant(d)
+
+    assert name(1024, 72, r4) == "gnca_b_mlp<16,128,1,24,24,4,4,8,1>"
+    assert name(128, 72, r4) == "gnca_b_mlp<16,128,1,24,24,4,4,8,1>"
+    assert name(96, 72, r4) == "gnca_b_mlp<16,128,1,24,24,4,4,8,1>"
+    assert name(128, 72, r4, gain=0.0) == "gnca_b_mlp<16,128,1,24,24,1,4,0,1>"
+    assert name(128, 72, [], graph=False) == "gnca_b_mlp<16,128,1,24,24,1,4,0,1>"
+    assert name(64, 72, r4) == "gnca_b_mlp<16,128,1,8,24,4,4,8,0>"
+    assert name(8, 72, r4) == "gnca_b_mlp<16,128,1,8,24,4,4,8,0>"
+    assert name(2, 72, r4) == "gnca_b_mlp<16,128,1,0,0,0,0,-1,0>"   # smaller tiles, runtime geometry
+    assert name(16, 40, r4) == "gnca_b_mlp<16,128,1,8,16,4,4,8,0>"
+    assert name(16, 40, r4, C=12).startswith("gnca_b_mlp<12,")
+    buf = ctypes.create_string_buffer(8)
+    assert lib.gnca_bb_variant(None, buf, 8) != 0
