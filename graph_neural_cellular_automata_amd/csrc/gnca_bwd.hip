@@ -655,6 +655,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     }
     if (msg && !uniform_w)
       for (int o = tid; o < k; o += kThreads) wts[o] = a.offw[(size_t)b * k + o];
+    BPROF_MARK(1);   // DMA issue
     for (int ti = wave; ti < TH; ti += NW) {
       if (lane < TW) {
         const int i = min(i0 + ti, H - 1), j = min(j0 + lane, W - 1);
@@ -662,7 +663,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
                                      a.sample_base, b, HW, (size_t)i * W + j) ? 1.f : 0.f;
       }
     }
-    BPROF_MARK(1);   // DMA issue + fire plane
+    BPROF_MARK(6);   // fire plane
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     BPROF_MARK(2);   // DMA wait

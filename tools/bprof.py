@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "build_ab")   # (travels to the GPU box; build_ablate is gpurun-ignored)
 LIB = os.path.join(OUT, "libgnca_prof.so")
-NAMES = ["weights", "dma_issue+fire", "dma_wait", "planes+compaction", "groups", "epilogue", "-", "loop_tail"]
+NAMES = ["weights", "dma_issue", "dma_wait", "planes+compaction", "groups", "epilogue", "fire", "loop_tail"]
 
 
 def build():
