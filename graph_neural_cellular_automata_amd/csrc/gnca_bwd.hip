@@ -346,7 +346,7 @@ __host__ __device__ inline BBLayout bb_layout(int CP, int HB, int TH, int TW, in
   L.sp = o; o += r4(L.RH * L.RW);
   L.kp = o; o += r4(TH * TW);
   L.lst = o; o += r4(TH * TW) + 8;   // compacted live-cell list + per-wave counts
-  L.w1f = o; o += MT * 64 * L.KSP;   // W1 fragments (GEMM1 recompute)
+  L.w1f = o; o += MT * (64 * L.KSP + (lean ? 12 : 0));   // W1 fragments (GEMM1 recompute; lean: row skew)
   L.w1t = o; o += lean ? 0 : FT * 64 * L.S1T;   // W1^T fragments (dY = W1^T dh)
   L.w2t = o; o += MT * 64 * L.S2T;   // W2^T fragments (dh = W2^T d_pre)
   L.wms = o; o += CPM * L.SWM;
@@ -395,6 +395,9 @@ struct BBArgs {
 // runtime C those tests were 64-bit lane masks held across the group loop (SGPR spills)
 // TH_ .. K_ (all > 0, K_ >= 0): the tile geometry and offset count at compile time (the planned
 // shapes of the C = 16 graph and classic steps, kBBS below): every LDS offset and loop bound a constant
+#ifndef GNCA_BB_W1SKEW
+#define GNCA_BB_W1SKEW 1      // the lean instances skew the W1 image's rows by 4 (lane >> 4) floats (A/B: 0)
+#endif
 // LL: the lean LDS layout (bb_layout's `lean`) of the large-tile instances
 template <int CP, int HB, bool FULL = false, int TH_ = 0, int TW_ = 0, int RY_ = 0, int RX_ = 0, int K_ = -1,
           bool LL = false>
@@ -404,6 +407,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   const int TH = TH_ ? TH_ : a.TH, TW = TW_ ? TW_ : a.TW, RY = RY_ ? RY_ : a.RY, RX = RX_ ? RX_ : a.RX;
   static_assert(!LL || (HB / 16) % 2 == 0, "lean layout: two halves of whole 16-unit tiles");
   const BBLayout L = bb_layout(CP, HB, TH, TW, RY, RX, K_ >= 0 ? K_ : a.k, LL);
+  constexpr bool W1SK = LL && GNCA_BB_W1SKEW;
   const int RH = L.RH, RW = L.RW, PSTR = L.PSTR, ALW = L.ALW;
   const int KSP = L.KSP, S1T = L.S1T, S2T = L.S2T, SWM = L.SWM, ST1 = L.ST1, ST2 = L.ST2, ST3 = L.ST3;
   float* xs = smem + L.xs;
@@ -480,7 +484,15 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       const int c = idx / 36, e = idx % 36, f = e / 12, tap = e % 12;
       return (c < C && tap < 9) ? a.perc[(3 * c + f) * 9 + tap] : 0.f;
     });
-    f1.store(w1f, tid);
+    if constexpr (LL && GNCA_BB_W1SKEW) {
+      // row (m, l) starts 12 m + 4 (l >> 4) floats late: dY's single-float reads of the image (LL below) then
+      // hit 64 distinct banks, GEMM1's 16-byte reads stay conflict-free (the skew is constant over
+      // each 16-lane quarter)
+      // (row block m: 64 KSP + 12 floats)
+      f1.store_map(w1f, tid, [&](int idx) { return idx + 12 * ((idx / cKSP) >> 6) + 4 * (((idx / cKSP) & 63) >> 4); });
+    } else {
+      f1.store(w1f, tid);
+    }
     if constexpr (!LL) f2.store(w1t, tid);
     f3.store(w2t, tid);
     f4_.store(wms, tid);
@@ -737,8 +749,40 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
     }
     BPROF_MARK(3);   // planes + compaction + dead-cell zero stores
 
+    // a group's U / dx loads (the GroupNorm-backward inputs of its cells)
+    auto load_ud = [&](int qq, float (&u_)[MO][4], float (&d_)[MO][4]) {
+      const int idx_ = 16 * qq + c16;
+      const bool valid_ = idx_ < nlive;
+      const int n_ = lst[valid_ ? idx_ : 0];
+      const int ti_ = n_ / TW, tj_ = n_ - (n_ / TW) * TW;
+      const int celli_ = (i0 + ti_) * W + (j0 + tj_);
+      const float keep_ = valid_ ? fp[n_] : 0.f;
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 16 * mo + 4 * g + r;
+          u_[mo][r] = 0.f;
+          d_[mo][r] = 0.f;
+          if (keep_ != 0.f && c < C) {
+#ifndef GNCA_BB_ABL_LOAD
+#define GNCA_BB_ABL_LOAD 0   // timing-only builds: 1 = U / dx not loaded (wrong results)
+#endif
+            if (GNCA_BB_ABL_LOAD) {
+              u_[mo][r] = 0.5f + 1e-3f * (float)celli_;
+              d_[mo][r] = 0.25f + 1e-3f * (float)c;
+            } else {
+              u_[mo][r] = Ub[c * HWi + celli_];
+              if (gn) d_[mo][r] = Db[c * HWi + celli_];
+            }
+          }
+        }
+    };
+    // (issuing the next group's loads once this group's were consumed, into 8 more registers, measured
+    //  1 % slower at B=1024: profiles/r06h_bb_pf_skew_ab.txt)
+    const int ngr = (nlive + 15) >> 4;
 #pragma unroll 1
-    for (int q = wave; q < ((nlive + 15) >> 4); q += NW) {
+    for (int q = wave; q < ngr; q += NW) {
       const int idx = 16 * q + c16;
       const bool valid = idx < nlive;
       const int n = lst[valid ? idx : 0];
@@ -749,18 +793,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       // issue this group's U / dx loads first: their latency hides under the recompute below
       const float keep = valid ? fp[n] : 0.f;   // invalid (padding) lanes contribute nothing
       float ul[MO][4], dl[MO][4];
-#pragma unroll
-      for (int mo = 0; mo < MO; ++mo)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = 16 * mo + 4 * g + r;
-          ul[mo][r] = 0.f;
-          dl[mo][r] = 0.f;
-          if (keep != 0.f && c < C) {
-            ul[mo][r] = Ub[c * HWi + celli];
-            if (gn) dl[mo][r] = Db[c * HWi + celli];
-          }
-        }
+      load_ud(q, ul, dl);
 
       // -- gather (recompute) --
       float gv[CPQ];
@@ -818,7 +851,8 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
       for (int s0 = 0; s0 < KS; s0 += 4) {
         f4 w4[MT];
 #pragma unroll
-        for (int m = 0; m < MT; ++m) w4[m] = *reinterpret_cast<const f4*>(w1f + (m * 64 + lane) * KSP + s0);
+        for (int m = 0; m < MT; ++m)
+          w4[m] = *reinterpret_cast<const f4*>(w1f + (m * 64 + lane) * KSP + s0 + (W1SK ? 12 * m + 4 * (lane >> 4) : 0));
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -883,7 +917,8 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
           if constexpr (LL) {
             // A[slot = 16ft + c16][hid = 16m + 4g + r] from the W1 image: W1[16m + (l & 15)][4s + (l >> 4)]
             // sits at w1f[(64m + l) KSP + s], here l = 4g + r + 16 (c16 & 3), s = 4ft + (c16 >> 2)
-            const float* wl = w1f + (4 * g + 16 * (c16 & 3)) * KSP + (c16 >> 2) + m * 64 * KSP;
+            const float* wl = w1f + (4 * g + 16 * (c16 & 3)) * KSP + (c16 >> 2) + m * 64 * KSP +
+                              (W1SK ? 12 * m + 4 * (c16 & 3) : 0);
 #pragma unroll
             for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
@@ -901,13 +936,22 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
 #ifndef GNCA_BB_ABL_STORE
 #define GNCA_BB_ABL_STORE 0   // timing-only builds: 1 = no dY / dG stores (wrong results)
 #endif
+#ifndef GNCA_BB_NT_STORE
+#define GNCA_BB_NT_STORE 0    // A/B builds: 1 = dY / dG written with nontemporal stores
+#endif
         if (valid && !GNCA_BB_ABL_STORE) {
           float* q = dYb + celli;
           if (first && cfull && 16 * FT == 3 * CP) {
 #pragma unroll
             for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) q[plo[ft][r]] = ay[ft][r];
+              for (int r = 0; r < 4; ++r) {
+#if GNCA_BB_NT_STORE
+                __builtin_nontemporal_store(ay[ft][r], q + plo[ft][r]);
+#else
+                q[plo[ft][r]] = ay[ft][r];
+#endif
+              }
           } else if (first) {
 #pragma unroll
             for (int ft = 0; ft < FT; ++ft)
@@ -951,7 +995,13 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
             float* q = dGb + (16 * mi + 4 * g) * HWi + celli;
             if (cfull && (CP & 15) == 0) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) q[r * HWi] = ag[r];
+              for (int r = 0; r < 4; ++r) {
+#if GNCA_BB_NT_STORE
+                __builtin_nontemporal_store(ag[r], q + r * HWi);
+#else
+                q[r * HWi] = ag[r];
+#endif
+              }
             } else {
 #pragma unroll
               for (int r = 0; r < 4; ++r)

@@ -193,6 +193,15 @@ struct RegFill {
       if (idx < N) dst[idx] = v[u];
     }
   }
+  // element idx to dst[map(idx)]
+  template <class M>
+  __device__ __forceinline__ void store_map(float* dst, int tid, M map) const {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = tid + u * NT;
+      if (idx < N) dst[map(idx)] = v[u];
+    }
+  }
 };
 
 // Sequential (fixed-order, bit-reproducible) sums of the pairs p[t*stride], p[t*stride+1],
