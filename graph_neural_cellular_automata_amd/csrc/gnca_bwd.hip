@@ -936,22 +936,14 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
 #ifndef GNCA_BB_ABL_STORE
 #define GNCA_BB_ABL_STORE 0   // timing-only builds: 1 = no dY / dG stores (wrong results)
 #endif
-#ifndef GNCA_BB_NT_STORE
-#define GNCA_BB_NT_STORE 0    // A/B builds: 1 = dY / dG written with nontemporal stores
-#endif
+// (nontemporal dY / dG stores measured slower: B=1024 backward 3.22 -> 3.46 ms, profiles/r06h_bb_ablations.txt)
         if (valid && !GNCA_BB_ABL_STORE) {
           float* q = dYb + celli;
           if (first && cfull && 16 * FT == 3 * CP) {
 #pragma unroll
             for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-#if GNCA_BB_NT_STORE
-                __builtin_nontemporal_store(ay[ft][r], q + plo[ft][r]);
-#else
-                q[plo[ft][r]] = ay[ft][r];
-#endif
-              }
+              for (int r = 0; r < 4; ++r) q[plo[ft][r]] = ay[ft][r];
           } else if (first) {
 #pragma unroll
             for (int ft = 0; ft < FT; ++ft)
@@ -995,13 +987,7 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
             float* q = dGb + (16 * mi + 4 * g) * HWi + celli;
             if (cfull && (CP & 15) == 0) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-#if GNCA_BB_NT_STORE
-                __builtin_nontemporal_store(ag[r], q + r * HWi);
-#else
-                q[r * HWi] = ag[r];
-#endif
-              }
+              for (int r = 0; r < 4; ++r) q[r * HWi] = ag[r];
             } else {
 #pragma unroll
               for (int r = 0; r < 4; ++r)
