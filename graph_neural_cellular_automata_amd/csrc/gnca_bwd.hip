@@ -380,6 +380,9 @@ struct BBArgs {
   // cells' dY / dG / dmb are not stored at all and their readers (BC, BC2) take them as zeros
   // from the keep plane; null (A/B builds): the dead cells' zeros are stored
   uint8_t* keep;
+  // masked step (torus): the active samples in order, their count at alist[B] (gnca_b_actlist), or
+  // null: the persistent grid then walks only the active samples' tiles, evenly over the workgroups
+  const int* alist;
   float* part;         // [gridDim.x * NW][npart]
   uint64_t seed;
   int64_t rng_step;
@@ -559,9 +562,11 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   const int nxcd = gridDim.x >= 8 ? 8 : 1;
   const int xg_ = blockIdx.x % nxcd, xr_ = blockIdx.x / nxcd;
   const int per_x = (int)(gridDim.x / nxcd) + ((int)(gridDim.x % nxcd) > xg_ ? 1 : 0);
-  const int tq = a.total_tiles / nxcd, trm = a.total_tiles % nxcd;
+  const int ntiles = a.alist ? a.alist[a.B] * a.tps : a.total_tiles;
+  const int tq = ntiles / nxcd, trm = ntiles % nxcd;
   const int t_begin = xg_ * tq + min(xg_, trm), t_end = t_begin + tq + (xg_ < trm ? 1 : 0);
-  for (int tile = t_begin + xr_; tile < t_end; tile += per_x) {
+  for (int vt = t_begin + xr_; vt < t_end; vt += per_x) {
+    const int tile = a.alist ? a.alist[vt / a.tps] * a.tps + vt % a.tps : vt;
     const int b = tile / a.tps, tin = tile - b * a.tps;
     const int ty = tin / a.tiles_x, tx = tin - ty * a.tiles_x;
     const int i0 = ty * TH, j0 = tx * TW;
@@ -1120,6 +1125,30 @@ __global__ __launch_bounds__(kThreads, 1) void gnca_b_mlp(const BBArgs a) {
   }
   BPROF_MARK(5);   // partial rows -> HBM
   BPROF_STORE;
+}
+
+// The active samples of a masked step in increasing order, their count at alist[B] (one workgroup;
+// ballot prefix sums, so the list does not depend on thread timing)
+__global__ __launch_bounds__(kThreads) void gnca_b_actlist(const uint8_t* active, int B, int* alist) {
+  __shared__ int wsum[NW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int base = 0;
+  for (int b0 = 0; b0 < B; b0 += kThreads) {
+    const int b = b0 + tid;
+    const bool on = b < B && active[b] != 0;
+    const uint64_t bal = __ballot(on);
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int off = base, tot = 0;
+    for (int u = 0; u < NW; ++u) {
+      off += u < w ? wsum[u] : 0;
+      tot += wsum[u];
+    }
+    if (on) alist[off + __popcll(bal & ((1ull << lane) - 1ull))] = b;
+    base += tot;
+    __syncthreads();
+  }
+  if (tid == 0) alist[B] = base;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1756,7 +1785,8 @@ struct BwdPlan {
   int nrb, rows_per;       // BC2
   size_t ldsD;
   int npart, o_w1, o_b1, o_w2, o_wm, o_bm, nq;
-  size_t off_fwd, off_U, off_dY, off_dG, off_dmb, off_keep, off_pa, off_coef, off_pb, off_dots, off_pq, off_corr, bytes;
+  size_t off_fwd, off_U, off_dY, off_dG, off_dmb, off_keep, off_alist, off_pa, off_coef, off_pb, off_dots, off_pq, off_corr,
+      bytes;
 };
 
 static int bwd_device_cus() {
@@ -1944,6 +1974,7 @@ static bool bwd_plan(const gnca_step_desc* d, BwdPlan* P, bool lean_ok = true) {
   P->off_dG = carve(P->msg ? n * 4 : 0);
   P->off_dmb = carve(P->msg && P->zp ? hw * 4 : 0);
   P->off_keep = carve(hw);
+  P->off_alist = carve((size_t)(d->B + 1) * 4);
   P->off_pa = carve((size_t)d->B * P->nbands * (2 + 2 * C) * 8);
   P->off_coef = carve((size_t)d->B * 4 * 4);
   P->off_pb = carve((size_t)P->gridB * NW * P->npart * 4);
@@ -2169,6 +2200,19 @@ int gnca_step_bwd_f32(const gnca_step_desc* desc, const gnca_weights* w, const f
 #endif
     const int RW = P.TW + 2 * P.RXB;
     for (int o = 0; o < a.k; ++o) a.odl[o] = d.offsets[2 * o] * RW + (P.zp ? 0 : d.offsets[2 * o + 1]);
+    // a masked step walks only the active samples' tiles (the static per-workgroup tile ranges of the
+    // full batch left the workgroups whose ranges held more active samples the slowest).  Not in
+    // zero-pad mode: BC2 reads every sample's keep bytes, which BB writes for the inactive ones
+#ifndef GNCA_BB_NO_ALIST   // A/B builds: the full batch's tile ranges (round 6 before the list)
+    if (active && !P.zp && keep) {
+#else
+    if (false) {
+#endif
+      int* alist = reinterpret_cast<int*>(wsb + P.off_alist);
+      hipLaunchKernelGGL(gnca_b_actlist, dim3(1), dim3(kThreads), 0, st, active, B, alist);
+      if ((rc = bwd_check()) != GNCA_OK) return rc;
+      a.alist = alist;
+    }
 #ifndef GNCA_BB_NO_DMA4   // A/B builds: 4-byte staging pieces (round 4's BB)
     if (W % 4 == 0 && P.RXB % 4 == 0 && P.TW % 4 == 0 && P.bbf32) a.flags |= kDma4;
 #endif
